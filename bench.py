@@ -1,0 +1,184 @@
+#!/usr/bin/env python3
+"""Benchmark: batched Board.step (BASELINE.json metric) on 1..8 MI355X.
+
+    python bench.py --gpus N --steps K --warmup W [--config c2|c3|c5]
+
+One "step" = one TileMatchEnv.step for every env of the shard (one HIP launch),
+uniform random actions pre-staged in HBM, autoreset on (num_moves = 30, so
+every 30th step also regenerates every board).  Each rank steps its own
+contiguous shard of envs (seed = global env index); there is no collective on
+the data path.  Rank 0 prints one JSON line.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+for _p in (ROOT, os.path.join(ROOT, "tile-match-gym_amd")):
+    if _p not in sys.path:
+        sys.path.insert(0, _p)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+METRIC = "env-steps/sec (whole node), 65536×10×10 boards, at 1/2/4/8 MI355X"
+HBM_PEAK_GBS = 8000.0           # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+
+CONFIGS = {
+    # name: (R, C, k, colourless, colour, boards per GPU, description)
+    "c2": (10, 10, 4, [], [], 65536, "65536 x 10x10 boards per GPU, 4 colours, no specials"),
+    "c3": (10, 10, 4, [], ["vertical_laser", "horizontal_laser", "bomb"], 262144,
+           "262144 x 10x10 boards per GPU, 4 colours, v/h-laser + bomb"),
+    "c5": (20, 20, 6, ["cookie"], ["vertical_laser", "horizontal_laser", "bomb"], 262144,
+           "262144 x 20x20 boards per GPU, 6 colours, all specials"),
+}
+
+
+def algorithmic_bytes_per_env_step(R, C):
+    """4RC (int8 colour+type read+write) + 48 (PCG64 state r/w
+    + inc read) + 8 (half-word buffer r/w) + 4 (action) + 8 (timer r/w)
+    + 16 (reward, n_new, n_act, flags) + 8*ceil(A/64) (effective mask)."""
+    A = 2 * R * C - R - C
+    return 4 * R * C + 48 + 8 + 4 + 8 + 16 + 8 * ((A + 63) // 64)
+
+
+def cpu_baseline(R, C, k, smask, moves, budget_s=12.0):
+    """The oracle (oracle/tmg_oracle.c, a bit-exact C port of the reference
+    Board) timed on this host's cores over a bounded sample of the same
+    workload (same seeds / action distribution)."""
+    from oracle import oracle as orc
+    from tile_match_gym_amd.seeding import batch_rng_words
+    threads = min(16, os.cpu_count() or 1)
+    n = 2048
+    o = orc.OracleBatch(R, C, k, smask, moves, batch_rng_words(range(n)), threads=threads)
+    o.reset()
+    A = 2 * R * C - R - C
+    rs = np.random.default_rng(12345)
+    acts = rs.integers(0, A, (moves, n)).astype(np.int32)
+    steps = 0
+    t0 = time.perf_counter()
+    while True:
+        for t in range(moves):
+            o.step(acts[t], autoreset=True)
+        steps += moves
+        el = time.perf_counter() - t0
+        if el >= budget_s:
+            break
+    return {"value": round(n * steps / el, 1), "unit": "env-steps/s", "cores": threads, "kind": "port",
+            "sample": f"{n} envs x {steps} steps ({steps // moves} episodes incl. autoreset), "
+                      f"{el:.1f} s, OpenMP over {threads} threads"}
+
+
+def load_traffic(config):
+    p = os.path.join(ROOT, "profiles", "traffic.json")
+    if not os.path.exists(p):
+        return None
+    try:
+        d = json.load(open(p))
+        return d.get(config, {}).get("hbm_bytes_per_launch")
+    except Exception:
+        return None
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=300)
+    ap.add_argument("--warmup", type=int, default=30)
+    ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
+    ap.add_argument("--boards", type=int, default=0, help="override boards per GPU")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local_rank)
+        dist.init_process_group("nccl")
+    else:
+        torch.cuda.set_device(0)
+    dev = torch.device("cuda", torch.cuda.current_device())
+
+    from tile_match_gym_amd.vec_env import TileMatchVecEnv
+    R, C, k, cl, co, nb, desc = CONFIGS[args.config]
+    if args.boards:
+        nb = args.boards
+    moves = 30
+    env = TileMatchVecEnv(nb, R, C, k, moves, cl, co, seeds=range(rank * nb, (rank + 1) * nb), device=dev,
+                          autoreset=True)
+    A = env.num_actions
+    T = 300
+    acts = torch.from_numpy(np.random.default_rng(12345 + rank).integers(0, A, (T, nb)).astype(np.int32)).to(dev)
+    env.reset()
+    for t in range(args.warmup):
+        env.step_raw(acts[t % T])
+    torch.cuda.synchronize()
+
+    stream = torch.cuda.current_stream()
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        ev[i][0].record(stream)
+        env.step_raw(acts[(args.warmup + i) % T])
+        ev[i][1].record(stream)
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    kern_ms = sum(a.elapsed_time(b) for a, b in ev) / max(1, args.steps)
+    flags = env.flags.cpu().numpy()
+    assert not (flags & 0xC0).any(), "error/overflow flag raised during the bench"
+    if dist:
+        tt = torch.tensor([el], dtype=torch.float64, device=dev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        el = float(tt.item())
+        kk = torch.tensor([kern_ms], dtype=torch.float64, device=dev)
+        dist.all_reduce(kk, op=dist.ReduceOp.MAX)
+        kern_ms = float(kk.item())
+
+    if rank == 0:
+        total = nb * world * args.steps
+        value = total / el
+        bpu = algorithmic_bytes_per_env_step(R, C)
+        achieved = bpu * nb / (kern_ms * 1e-3) / 1e9
+        smask = (1 if "cookie" in cl else 0) | (2 if "vertical_laser" in co else 0) | \
+                (4 if "horizontal_laser" in co else 0) | (8 if "bomb" in co else 0)
+        cpu = None if (args.no_cpu_baseline or world > 1) else cpu_baseline(R, C, k, smask, moves)
+        out = {
+            "metric": METRIC,
+            "value": round(value, 1),
+            "unit": "env-steps/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(el * 1e3 / args.steps, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "int8",
+            "data": "synthetic (uniform random actions from default_rng(12345); seeds = global env index)",
+            "config": {"workload": f"{args.config}: {desc}, num_moves=30, autoreset",
+                       "boards_per_gpu": nb, "rows": R, "cols": C, "colours": k,
+                       "specials": cl + co, "parallelism": f"dp{world} (independent env shards, no collective)"},
+            "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(achieved / HBM_PEAK_GBS, 6), "traffic": load_traffic(args.config),
+                         "kernel_ms_per_launch": round(kern_ms, 4), "algorithmic_bytes_per_env_step": bpu},
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(out), flush=True)
+    if dist:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

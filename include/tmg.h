@@ -1,0 +1,109 @@
+/*
+ * tmg.h — C ABI of libtmg.so, the MI355X (gfx950) batched tile-match Board.
+ *
+ * The reference (akshilpatel/tile-match-gym v1.0.6) has no FFI: its hot path is
+ * the Python class API below, and this ABI is what a binding of that path
+ * binds (the ctypes stub lives in tile_match_gym_amd/_native.py; see
+ * INTEGRATION.md).  Each entry point cites the reference interface it replaces.
+ *
+ * Batched state (device memory, owned by the caller, e.g. PyTorch tensors):
+ *   board  int8   [n][2][R][C]   plane 0 colour (0 empty/colourless, 1..k),
+ *                                plane 1 type (0 empty, 1 normal, 2 v-laser,
+ *                                3 h-laser, 4 bomb, -1 cookie)   board.py:18-25,96
+ *   rng    uint64 [n][5]         numpy PCG64 per env: state lo/hi, inc lo/hi,
+ *                                has_uint32<<32 | uinteger       tile_match_env.py:49
+ *   timer  int32  [n]            moves taken this episode         tile_match_env.py:88,100
+ *   eff    uint64 [n][W]         effective-action bitmask, W = ceil(A/64),
+ *                                A = 2RC-R-C; bit a of word a/64  tile_match_env.py:118-124
+ * Per-step outputs (device memory):
+ *   reward int32 [n]   num_eliminations                            board.py:330-395
+ *   n_new  int32 [n]   info["num_new_specials"]
+ *   n_act  int32 [n]   info["num_specials_activated"]
+ *   flags  uint8 [n]   bit0 done, bit1 is_combination_match, bit2 shuffled,
+ *                      bit3 autoreset ran, bit6 internal capacity overflow,
+ *                      bit7 error (step after done / bad action) tile_match_env.py:94-95
+ *
+ * Errors: 0 = ok, negative = error; tmg_last_error() gives a thread-local
+ * message.  All launches are asynchronous on `stream` (a hipStream_t; NULL =
+ * default stream).  Not re-entrant per context.
+ */
+#ifndef TMG_H
+#define TMG_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct tmg_ctx tmg_ctx;
+
+#if defined(__GNUC__) || defined(__clang__)
+#define TMG_API __attribute__((visibility("default")))
+#else
+#define TMG_API
+#endif
+
+/* Special-tile mask bits (Board(colourless_specials=..., colour_specials=...), board.py:42-61). */
+#define TMG_SPECIAL_COOKIE 1u
+#define TMG_SPECIAL_VLASER 2u
+#define TMG_SPECIAL_HLASER 4u
+#define TMG_SPECIAL_BOMB   8u
+
+#define TMG_FLAG_DONE      0x01u
+#define TMG_FLAG_COMBO     0x02u
+#define TMG_FLAG_SHUFFLED  0x04u
+#define TMG_FLAG_RESET     0x08u
+#define TMG_FLAG_OVERFLOW  0x40u
+#define TMG_FLAG_ERROR     0x80u
+
+/* Replaces TileMatchEnv.__init__ / Board.__init__ (tile_match_env.py:17-77,
+ * board.py:42-93): fixes the shape, colours, specials and episode length for a
+ * batch, builds the action->coords table (board.py:77-93) and the PCG64
+ * jump-ahead table on `device`. */
+TMG_API int tmg_create(tmg_ctx **out, int device, int rows, int cols, int colours,
+               uint32_t specials_mask, int num_moves);
+
+/* Frees the context's device tables.  Never frees caller buffers. */
+TMG_API int tmg_destroy(tmg_ctx *ctx);
+
+/* Replaces TileMatchEnv.reset (tile_match_env.py:84-91 -> Board.generate_board,
+ * board.py:95-131) for every env i with env_mask == NULL or env_mask[i] != 0:
+ * generates a board from the env's RNG stream (continuing it, like reset()
+ * without a seed), sets timer = 0 and writes the effective-action mask. */
+TMG_API int tmg_reset(tmg_ctx *ctx, int64_t n, int8_t *board, uint64_t *rng, int32_t *timer,
+              uint64_t *eff, const uint8_t *env_mask, void *stream);
+
+/* Replaces TileMatchEnv.step (tile_match_env.py:93-112 -> Board.move,
+ * board.py:330-395) for n envs at once.  actions[i] in [0, A).
+ * trust_eff != 0: eff holds the mask this library produced for the current
+ *   boards (the effectiveness test of board.py:352 is then a bit lookup);
+ *   pass 0 after editing boards by hand.
+ * autoreset != 0: an env whose episode ends is regenerated in the same call
+ *   (continuing its RNG stream, == reset() without a seed); reward / flags
+ *   still describe the final move and flag bit3 is set.  With autoreset == 0
+ *   a finished env writes an all-zero eff mask (tile_match_env.py:119-120) and
+ *   a further step sets TMG_FLAG_ERROR without touching its state. */
+TMG_API int tmg_step(tmg_ctx *ctx, int64_t n, int8_t *board, uint64_t *rng, int32_t *timer,
+             const int32_t *actions, int32_t *reward, int32_t *n_new, int32_t *n_act,
+             uint8_t *flags, uint64_t *eff, int trust_eff, int autoreset, void *stream);
+
+/* Replaces TileMatchEnv._get_effective_actions (tile_match_env.py:118-124,
+ * is_move_effective board.py:735-787) as a bitmask, ignoring the timer. */
+TMG_API int tmg_effective(tmg_ctx *ctx, int64_t n, const int8_t *board, uint64_t *eff, void *stream);
+
+/* Number of actions A = 2RC - R - C (tile_match_env.py:58) and mask words W. */
+TMG_API int tmg_num_actions(const tmg_ctx *ctx);
+TMG_API int tmg_mask_words(const tmg_ctx *ctx);
+
+/* Message for the last failing call on this thread. */
+TMG_API const char *tmg_last_error(void);
+
+/* ABI version (bumped on any signature change). */
+TMG_API int tmg_abi_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* TMG_H */

@@ -1,0 +1,1147 @@
+// tmg_board.hip — the batched tile-match Board on MI355X (gfx950).
+//
+// One wavefront (64 lanes) owns one board.  The board's int8 colour/type
+// planes live in LDS for the whole call; lanes map to cells for the
+// data-parallel stages (line flags, effective-action scan, refill, colour
+// regeneration, shuffle apply), to columns for gravity, and to 64
+// consecutive PCG64 outputs for random draws.  The order-dependent list logic
+// of the reference (get_colour_lines' perpendicular pass, process_colour_lines,
+// special placement, the recursive activate_special DFS, combination_match)
+// runs on lane 0 against LDS with an explicit stack.  With no specials enabled
+// the whole cascade stays wave-parallel (no lane-0 section).
+//
+// Reference: akshilpatel/tile-match-gym v1.0.6, src/tile_match_gym/board.py
+// and tile_match_env.py (file:line cited per function).  Bit-exact per seed.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "pcg64.h"
+
+namespace tmg {
+
+#ifndef TMG_WPB
+#define TMG_WPB 1          // waves (boards) per workgroup
+#endif
+
+#if TMG_WPB == 1
+#define WSYNC() __syncthreads()
+#else
+#define WSYNC()                                                  \
+    do {                                                         \
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");   \
+        __builtin_amdgcn_wave_barrier();                         \
+    } while (0)
+#endif
+
+enum : int { SP_COOKIE = 1, SP_VLASER = 2, SP_HLASER = 4, SP_BOMB = 8 };
+enum : int { M_NORMAL = 0, M_VLASER = 1, M_HLASER = 2, M_BOMB = 3, M_COOKIE = 4 };
+enum : int { FL_DONE = 1, FL_COMBO = 2, FL_SHUF = 4, FL_RESET = 8, FL_OVF = 0x40, FL_ERR = 0x80 };
+
+struct Params {
+    int R, C, N, A, W, k, smask, num_moves;
+    uint32_t thr;                 // Lemire threshold (2^32 - k) % k; 0 for powers of two
+    const uint64_t *jump;         // [64][4] jump-ahead table
+};
+
+// scalar slots in LDS
+enum : int { SC_NACT = 0, SC_NNEW, SC_ERR, SC_NZ, SC_A, SC_B, SC_C, SC_D, SC_COUNT = 16 };
+
+template <int MAXN>
+struct Ws {
+    static constexpr int POOL = 4 * MAXN + 256;     // coords of lines
+    static constexpr int MLINES = MAXN + 64;        // lines
+    static constexpr int MQ = 2 * MAXN + 64;        // process queue
+    static constexpr int MM = MAXN + 32;            // matches
+    static constexpr int MPOOL = 4 * MAXN + 256;    // coords of matches
+    static constexpr int MAXW = (2 * MAXN) / 64 + 2;
+    static constexpr int MSTK = MAXN + 8;
+
+    uint64_t rng[5];
+    uint64_t effw[MAXW];
+    int32_t sc[SC_COUNT];
+    uint32_t draw[MAXN + 128];
+    int8_t brd[2 * MAXN];          // [colour plane N][type plane N], runtime N
+    int8_t tmp[2 * MAXN];
+    uint8_t mark[MAXN];
+    uint8_t flag[MAXN];
+    int16_t perm[MAXN];
+    // lane-0 list machinery (general path)
+    int16_t pool[POOL];
+    int16_t ls[MLINES], ll[MLINES];
+    int16_t q[MQ];
+    int16_t mpool[MPOOL];
+    int16_t ms[MM], mlen[MM];
+    int8_t mname[MM], mcol[MM];
+    int16_t fcell[MSTK], fidx[MSTK];
+    int8_t ftype[MSTK], faux[MSTK];
+};
+
+__device__ inline uint64_t lanemask_lt(int lane) { return lane ? (~0ULL >> (64 - lane)) : 0ULL; }
+
+__device__ inline uint64_t rdlane64(uint64_t v, int l) {
+    uint32_t lo = __builtin_amdgcn_readlane((uint32_t)v, l);
+    uint32_t hi = __builtin_amdgcn_readlane((uint32_t)(v >> 32), l);
+    return ((uint64_t)hi << 32) | lo;
+}
+
+struct LaneJump {
+    U128 Aj, Gj;    // A^{lane+1}, G_{lane+1}
+};
+
+// --------------------------------------------------------------- RNG (LDS state)
+template <int MAXN>
+__device__ inline uint64_t s_next64(Ws<MAXN> &w) {                 // lane-0 serial
+    U128 s{w.rng[0], w.rng[1]}, inc{w.rng[2], w.rng[3]};
+    s = add128(mul128(s, U128{PCG_A_LO, PCG_A_HI}), inc);
+    w.rng[0] = s.lo;
+    w.rng[1] = s.hi;
+    return xsl_rr(s);
+}
+template <int MAXN>
+__device__ inline uint32_t s_next32(Ws<MAXN> &w) {
+    uint64_t h = w.rng[4];
+    if (h >> 32) { w.rng[4] = (uint32_t)h; return (uint32_t)h; }
+    uint64_t n = s_next64(w);
+    w.rng[4] = (1ULL << 32) | (n >> 32);
+    return (uint32_t)n;
+}
+template <int MAXN>
+__device__ inline int s_colour(const Params &P, Ws<MAXN> &w) {     // integers(1,k+1) one draw
+    uint32_t excl = (uint32_t)P.k;
+    uint64_t m = (uint64_t)s_next32(w) * excl;
+    uint32_t left = (uint32_t)m;
+    if (left < excl) {
+        while (left < P.thr) { m = (uint64_t)s_next32(w) * excl; left = (uint32_t)m; }
+    }
+    return 1 + (int)(m >> 32);
+}
+template <int MAXN>
+__device__ inline uint32_t s_interval(Ws<MAXN> &w, uint32_t max) { // random_interval
+    if (max == 0) return 0;
+    uint32_t mask = max;
+    mask |= mask >> 1; mask |= mask >> 2; mask |= mask >> 4; mask |= mask >> 8; mask |= mask >> 16;
+    uint32_t v;
+    while ((v = (s_next32(w) & mask)) > max) {}
+    return v;
+}
+
+// w.draw[0..M) <- M colours exactly as Generator.integers(1, k+1, M) (board.py:97,129,239)
+template <int MAXN>
+__device__ void draw_colours(const Params &P, Ws<MAXN> &w, int lane, const LaneJump &J, int M) {
+    if (M <= 0) return;
+    if (P.k == 1) {                                        // rng == 0: numpy draws nothing
+        for (int i = lane; i < M; i += 64) w.draw[i] = 1;
+        WSYNC();
+        return;
+    }
+    const uint64_t s0lo = w.rng[0], s0hi = w.rng[1], ilo = w.rng[2], ihi = w.rng[3], h0 = w.rng[4];
+    const int has = (int)(h0 >> 32) & 1;
+    int off = 0;
+    if (has) { if (lane == 0) w.draw[0] = (uint32_t)h0; off = 1; }
+    const int need = M - off;
+    const int n64 = (need + 1) >> 1;
+    U128 s{s0lo, s0hi};
+    const U128 incG = mul128(U128{ilo, ihi}, J.Gj);
+    uint64_t last_hi = (uint32_t)h0;
+    for (int base = 0; base < n64; base += 64) {
+        U128 sj = add128(mul128(J.Aj, s), incG);
+        uint64_t out = xsl_rr(sj);
+        int j = base + lane;
+        if (j < n64) {
+            int i0 = off + 2 * j;
+            w.draw[i0] = (uint32_t)out;
+            if (2 * j + 1 < need) w.draw[i0 + 1] = (uint32_t)(out >> 32);
+        }
+        int cnt = n64 - base < 64 ? n64 - base : 64;
+        s.lo = rdlane64(sj.lo, cnt - 1);
+        s.hi = rdlane64(sj.hi, cnt - 1);
+        last_hi = rdlane64(out >> 32, cnt - 1);
+    }
+    WSYNC();
+    // Lemire rejection (numpy buffered_bounded_lemire_uint32): vanishingly rare
+    bool rej = false;
+    if (P.thr) {
+        for (int i = lane; i < M; i += 64) {
+            uint32_t left = (uint32_t)((uint64_t)w.draw[i] * (uint32_t)P.k);
+            rej |= left < P.thr;
+        }
+    }
+    if (__ballot(rej) != 0ULL) {
+        if (lane == 0) {                                   // exact serial replay
+            w.rng[0] = s0lo; w.rng[1] = s0hi; w.rng[4] = h0;
+            for (int i = 0; i < M; i++) w.draw[i] = (uint32_t)s_colour(P, w);
+        }
+        WSYNC();
+        return;
+    }
+    for (int i = lane; i < M; i += 64) w.draw[i] = 1u + (uint32_t)(((uint64_t)w.draw[i] * (uint32_t)P.k) >> 32);
+    if (lane == 0) {
+        if (n64 > 0) {
+            w.rng[0] = s.lo; w.rng[1] = s.hi;
+            w.rng[4] = ((uint64_t)(need & 1) << 32) | (uint32_t)last_hi;
+        } else {
+            w.rng[4] = (uint32_t)h0;                       // only the buffered half was used
+        }
+    }
+    WSYNC();
+}
+
+// --------------------------------------------------------------- board helpers
+__device__ inline void action_coords(int R, int C, int a, int &r1, int &c1, int &r2, int &c2) {  // board.py:77-93
+    if (a < C * (R - 1)) { r1 = a / C; c1 = a % C; r2 = r1 + 1; c2 = c1; }
+    else { int i = a - C * (R - 1); r1 = i / (C - 1); c1 = i % (C - 1); r2 = r1; c2 = c1 + 1; }
+}
+
+template <int MAXN>
+__device__ inline void load_board(const Params &P, Ws<MAXN> &w, int lane, const int8_t *src) {
+    const int nb = 2 * P.N;
+    if ((nb & 3) == 0) {
+        const uint32_t *s = reinterpret_cast<const uint32_t *>(src);
+        uint32_t *d = reinterpret_cast<uint32_t *>(w.brd);
+        for (int i = lane; i < (nb >> 2); i += 64) d[i] = s[i];
+    } else {
+        for (int i = lane; i < nb; i += 64) w.brd[i] = src[i];
+    }
+}
+template <int MAXN>
+__device__ inline void store_board(const Params &P, const Ws<MAXN> &w, int lane, int8_t *dst) {
+    const int nb = 2 * P.N;
+    if ((nb & 3) == 0) {
+        uint32_t *d = reinterpret_cast<uint32_t *>(dst);
+        const uint32_t *s = reinterpret_cast<const uint32_t *>(w.brd);
+        for (int i = lane; i < (nb >> 2); i += 64) d[i] = s[i];
+    } else {
+        for (int i = lane; i < nb; i += 64) dst[i] = w.brd[i];
+    }
+}
+
+// is_move_effective, board.py:735-787 — exact windowed scan (any board)
+template <int MAXN>
+__device__ bool eff_exact(const Params &P, const Ws<MAXN> &w, int a) {
+    const int R = P.R, C = P.C, N = P.N;
+    int r1, c1, r2, c2;
+    action_coords(R, C, a, r1, c1, r2, c2);
+    const int8_t *col = w.brd, *typ = w.brd + N;
+    const int p = r1 * C + c1, q = r2 * C + c2;
+    const int tp = typ[p], tq = typ[q];
+    if ((tp != 0 && tp != 1) && (tq != 0 && tq != 1)) return true;
+    if (tp < 0 || tq < 0) return true;
+    const int cp = col[p], cq = col[q];
+    auto CO = [&](int x) -> int { return x == p ? cq : (x == q ? cp : (int)col[x]); };
+    auto TY = [&](int x) -> int { return x == p ? tq : (x == q ? tp : (int)typ[x]); };
+    int rmin = (r1 < r2 ? r1 : r2) - 2; if (rmin < 0) rmin = 0;
+    int rmax = (r1 > r2 ? r1 : r2) + 2; if (rmax > R - 1) rmax = R - 1;
+    int cmin = (c1 < c2 ? c1 : c2) - 2; if (cmin < 0) cmin = 0;
+    int cmax = (c1 > c2 ? c1 : c2) + 2; if (cmax > C - 1) cmax = C - 1;
+    if (cmin + 2 <= cmax)
+        for (int r = rmin; r <= rmax; r++)
+            for (int c = cmin; c + 2 <= cmax; c++) {
+                int x = r * C + c;
+                int a0 = CO(x);
+                if (a0 == CO(x + 1) && a0 == CO(x + 2) && TY(x + 2) >= 0) return true;
+            }
+    if (rmin + 2 <= rmax)
+        for (int r = rmin; r + 2 <= rmax; r++)
+            for (int c = cmin; c <= cmax; c++) {
+                int x = r * C + c;
+                int a0 = CO(x);
+                if (a0 == CO(x + C) && a0 == CO(x + 2 * C) && TY(x + 2 * C) >= 0) return true;
+            }
+    return false;
+}
+
+// Same predicate when the board holds no cookie and no pre-existing colour
+// triple (checked by the caller): only triples through exactly one of the two
+// swapped cells can appear, all inside the reference's window.
+template <int MAXN>
+__device__ bool eff_fast(const Params &P, const Ws<MAXN> &w, int a) {
+    const int R = P.R, C = P.C, N = P.N;
+    int r1, c1, r2, c2;
+    action_coords(R, C, a, r1, c1, r2, c2);
+    const int8_t *col = w.brd, *typ = w.brd + N;
+    const int p = r1 * C + c1, q = r2 * C + c2;
+    const int tp = typ[p], tq = typ[q];
+    if ((tp != 0 && tp != 1) && (tq != 0 && tq != 1)) return true;
+    const int x1 = col[p], x2 = col[q];
+    auto eq = [&](int r, int c, int x) -> bool { return r >= 0 && r < R && c >= 0 && c < C && col[r * C + c] == x; };
+    if (r2 == r1 + 1) {       // vertical pair: p (top) receives x2, q (bottom) receives x1
+        if (eq(r1 - 1, c1, x2) && eq(r1 - 2, c1, x2)) return true;
+        if (eq(r1, c1 - 1, x2) && (eq(r1, c1 - 2, x2) || eq(r1, c1 + 1, x2))) return true;
+        if (eq(r1, c1 + 1, x2) && eq(r1, c1 + 2, x2)) return true;
+        if (eq(r2 + 1, c1, x1) && eq(r2 + 2, c1, x1)) return true;
+        if (eq(r2, c1 - 1, x1) && (eq(r2, c1 - 2, x1) || eq(r2, c1 + 1, x1))) return true;
+        if (eq(r2, c1 + 1, x1) && eq(r2, c1 + 2, x1)) return true;
+    } else {                  // horizontal pair: p (left) receives x2, q (right) receives x1
+        if (eq(r1, c1 - 1, x2) && eq(r1, c1 - 2, x2)) return true;
+        if (eq(r1 - 1, c1, x2) && (eq(r1 - 2, c1, x2) || eq(r1 + 1, c1, x2))) return true;
+        if (eq(r1 + 1, c1, x2) && eq(r1 + 2, c1, x2)) return true;
+        if (eq(r1, c2 + 1, x1) && eq(r1, c2 + 2, x1)) return true;
+        if (eq(r1 - 1, c2, x1) && (eq(r1 - 2, c2, x1) || eq(r1 + 1, c2, x1))) return true;
+        if (eq(r1 + 1, c2, x1) && eq(r1 + 2, c2, x1)) return true;
+    }
+    return false;
+}
+
+// _get_effective_actions / possible_move (tile_match_env.py:118-124, board.py:558-569):
+// fills w.effw, returns whether any action is effective.
+template <int MAXN>
+__device__ bool scan_effective(const Params &P, Ws<MAXN> &w, int lane) {
+    const int R = P.R, C = P.C, N = P.N;
+    const int8_t *col = w.brd, *typ = w.brd + N;
+    bool odd = false;          // cookie on board or a pre-existing triple -> exact scan
+    for (int p = lane; p < N; p += 64) {
+        int r = p / C, c = p - r * C, x = col[p];
+        odd |= typ[p] < 0;
+        odd |= (c + 2 < C) && col[p + 1] == x && col[p + 2] == x && typ[p + 2] >= 0;
+        odd |= (r + 2 < R) && col[p + C] == x && col[p + 2 * C] == x && typ[p + 2 * C] >= 0;
+    }
+    const bool exact = __ballot(odd) != 0ULL;
+    uint64_t any = 0;
+    for (int base = 0, wi = 0; base < P.A; base += 64, wi++) {
+        int a = base + lane;
+        bool e = false;
+        if (a < P.A) e = exact ? eff_exact(P, w, a) : eff_fast(P, w, a);
+        uint64_t m = __ballot(e);
+        if (lane == 0) w.effw[wi] = m;
+        any |= m;
+    }
+    WSYNC();
+    return any != 0ULL;
+}
+
+// Line flags (get_colour_lines' first pass, board.py:158-193):
+// flag bit0 = vertical line anchored here, bit1 = horizontal line may start here.
+// Returns the bottom-most row holding a line, or -1.
+template <int MAXN>
+__device__ int detect_row(const Params &P, Ws<MAXN> &w, int lane) {
+    const int R = P.R, C = P.C, N = P.N;
+    const int8_t *col = w.brd, *typ = w.brd + N;
+    int pmax = -1;
+    for (int p0 = 0; p0 < N; p0 += 64) {
+        int p = p0 + lane;
+        uint8_t f = 0;
+        if (p < N) {
+            int r = p / C, c = p - r * C, x = col[p];
+            bool t = typ[p] > 0;
+            if (t && r >= 2 && col[p - C] == x && col[p - 2 * C] == x) f |= 1;
+            if (t && c + 2 < C && col[p + 1] == x && col[p + 2] == x) f |= 2;
+            w.flag[p] = f;
+        }
+        uint64_t m = __ballot(f != 0);
+        if (m) pmax = p0 + 63 - __clzll(m);
+    }
+    WSYNC();
+    (void)R;
+    return pmax < 0 ? -1 : pmax / C;
+}
+
+// For remove_colour_lines (board.py:120-131): row of the first coord of the
+// first line get_colour_lines would return, or -1 when it returns [].
+template <int MAXN>
+__device__ int first_line_row(const Params &P, Ws<MAXN> &w, int lane) {
+    const int C = P.C;
+    const int rs = detect_row(P, w, lane);
+    if (rs < 0) return -1;
+    uint8_t f = lane < C ? w.flag[rs * C + lane] : 0;
+    uint64_t mrow = __ballot(f != 0);
+    int c0 = __ffsll((unsigned long long)mrow) - 1;
+    int fc0 = __builtin_amdgcn_readfirstlane((int)w.flag[rs * C + c0]);
+    if (!(fc0 & 1)) return rs;                            // horizontal line at (rs, c0..)
+    // vertical: the line starts at the top of the same-colour run above rs
+    const int8_t *col = w.brd;
+    int x = col[rs * C + c0];
+    bool neq = lane < rs && col[lane * C + c0] != x;
+    uint64_t mn = __ballot(neq);
+    return mn ? (63 - __clzll(mn)) + 1 : 0;
+}
+
+// gravity, board.py:217-229 — one lane per column, stable partition
+template <int MAXN>
+__device__ void gravity(const Params &P, Ws<MAXN> &w, int lane) {
+    const int R = P.R, C = P.C, N = P.N;
+    int8_t *col = w.brd, *typ = w.brd + N;
+    if (lane < C) {
+        int wr = R - 1;
+        for (int r = R - 1; r >= 0; r--) {
+            int p = r * C + lane;
+            int8_t a = col[p], t = typ[p];
+            if (!(a == 0 && t == 0)) {
+                int d = wr * C + lane;
+                col[d] = a; typ[d] = t;
+                wr--;
+            }
+        }
+        for (int r = wr; r >= 0; r--) { col[r * C + lane] = 0; typ[r * C + lane] = 0; }
+    }
+    WSYNC();
+}
+
+// refill, board.py:231-241 — empties in row-major order get consecutive draws
+template <int MAXN>
+__device__ void refill(const Params &P, Ws<MAXN> &w, int lane, const LaneJump &J) {
+    const int N = P.N;
+    int8_t *col = w.brd, *typ = w.brd + N;
+    int total = 0;
+    for (int p0 = 0; p0 < N; p0 += 64) {
+        int p = p0 + lane;
+        bool e = p < N && col[p] == 0 && typ[p] == 0;
+        total += __popcll(__ballot(e));
+    }
+    if (total == 0) return;
+    draw_colours(P, w, lane, J, total);
+    int base = 0;
+    for (int p0 = 0; p0 < N; p0 += 64) {
+        int p = p0 + lane;
+        bool e = p < N && col[p] == 0 && typ[p] == 0;
+        uint64_t m = __ballot(e);
+        if (e) {
+            int idx = base + __popcll(m & lanemask_lt(lane));
+            col[p] = (int8_t)w.draw[idx];
+            typ[p] = 1;
+        }
+        base += __popcll(m);
+    }
+    WSYNC();
+}
+
+// shuffle, board.py:114-118
+template <int MAXN>
+__device__ void shuffle(const Params &P, Ws<MAXN> &w, int lane) {
+    const int N = P.N;
+    if (lane == 0) {
+        for (int i = 0; i < N; i++) w.perm[i] = (int16_t)i;
+        for (int i = N - 1; i >= 1; i--) {
+            int j = (int)s_interval(w, (uint32_t)i);
+            int16_t x = w.perm[i]; w.perm[i] = w.perm[j]; w.perm[j] = x;
+        }
+    }
+    for (int i = lane; i < 2 * N; i += 64) w.tmp[i] = w.brd[i];
+    WSYNC();
+    for (int p = lane; p < N; p += 64) {
+        int s = w.perm[p];
+        w.brd[p] = w.tmp[s];
+        w.brd[N + p] = w.tmp[N + s];
+    }
+    WSYNC();
+}
+
+// generate_board's / move's "while not possible_move() or lines" loop
+// (board.py:102-109, 381-391, remove_colour_lines :120-131).  Leaves the final
+// board's effective mask in w.effw.  Returns true when a shuffle ran.
+template <int MAXN>
+__device__ bool ensure_playable(const Params &P, Ws<MAXN> &w, int lane, const LaneJump &J) {
+    bool shuffled = false;
+    for (;;) {
+        for (;;) {
+            int r0 = first_line_row(P, w, lane);
+            if (r0 < 0) break;
+            int row = P.R - 1 < r0 + 1 ? P.R - 1 : r0 + 1;
+            int M = (row + 1) * P.C;
+            draw_colours(P, w, lane, J, M);
+            for (int p = lane; p < M; p += 64) w.brd[p] = (int8_t)w.draw[p];
+            WSYNC();
+        }
+        if (scan_effective(P, w, lane)) break;
+        shuffle(P, w, lane);
+        shuffled = true;
+    }
+    return shuffled;
+}
+
+// generate_board, board.py:95-109
+template <int MAXN>
+__device__ void generate_board(const Params &P, Ws<MAXN> &w, int lane, const LaneJump &J) {
+    const int N = P.N;
+    draw_colours(P, w, lane, J, N);
+    for (int p = lane; p < N; p += 64) { w.brd[p] = (int8_t)w.draw[p]; w.brd[N + p] = 1; }
+    WSYNC();
+    ensure_playable(P, w, lane, J);
+}
+
+template <int MAXN>
+__device__ int count_type_zero(const Params &P, Ws<MAXN> &w, int lane) {
+    int z = 0;
+    for (int p0 = 0; p0 < P.N; p0 += 64) {
+        int p = p0 + lane;
+        z += __popcll(__ballot(p < P.N && w.brd[P.N + p] == 0));
+    }
+    return z;
+}
+
+template <int MAXN>
+__device__ int count_colour_nonzero(const Params &P, Ws<MAXN> &w, int lane) {
+    int z = 0;
+    for (int p0 = 0; p0 < P.N; p0 += 64) {
+        int p = p0 + lane;
+        z += __popcll(__ballot(p < P.N && w.brd[p] != 0));
+    }
+    return z;
+}
+
+// ---------------------------------------------------------------- fast cascade
+// One cascade iteration when no special can exist (no specials enabled and
+// every type is 1): the reference then turns every line of
+// get_colour_lines (first pass + perpendicular pass, board.py:149-215) into a
+// normal match (process_colour_lines :269-327) and clears their union
+// (resolve_colour_match :460-471).  Returns the number of cleared cells.
+template <int MAXN>
+__device__ int fast_clear(const Params &P, Ws<MAXN> &w, int lane, int rs) {
+    const int R = P.R, C = P.C, N = P.N;
+    int8_t *col = w.brd, *typ = w.brd + N;
+    // mark bit0: first-pass coord (static coords list), bit1: cleared
+    for (int p = lane; p < N; p += 64) w.mark[p] = 0;
+    WSYNC();
+    // horizontal: cells of row rs inside a same-colour run of length >= 3
+    {
+        bool e = lane + 1 < C && col[rs * C + lane] == col[rs * C + lane + 1];
+        uint64_t em = __ballot(e);
+        uint64_t t = em & (em >> 1);
+        uint64_t cov = t | (t << 1) | (t << 2);
+        if (lane < C && ((cov >> lane) & 1)) w.mark[rs * C + lane] = 3;
+    }
+    // vertical: runs of length >= 3 whose bottom is row rs
+    {
+        uint8_t f = lane < C ? w.flag[rs * C + lane] : 0;
+        uint64_t vm = __ballot(f & 1);
+        while (vm) {
+            int c = __ffsll((unsigned long long)vm) - 1;
+            vm &= vm - 1;
+            int x = col[rs * C + c];
+            bool neq = lane < rs && col[lane * C + c] != x;
+            uint64_t mn = __ballot(neq);
+            int top = mn ? (63 - __clzll(mn)) + 1 : 0;
+            if (lane >= top && lane <= rs) w.mark[lane * C + c] = 3;
+        }
+    }
+    WSYNC();
+    // perpendicular pass: from every first-pass coord walk both axes over
+    // non-coord cells of the same colour; a run of >= 3 is a line
+    for (int p = lane; p < N; p += 64) {
+        if (!(w.mark[p] & 1)) continue;
+        int r = p / C, c = p - r * C, x = col[p];
+        int lft = 0, rgt = 0, up = 0, dn = 0;
+        while (c - lft - 1 >= 0 && !(w.mark[p - lft - 1] & 1) && col[p - lft - 1] == x) lft++;
+        while (c + rgt + 1 < C && !(w.mark[p + rgt + 1] & 1) && col[p + rgt + 1] == x) rgt++;
+        while (r - up - 1 >= 0 && !(w.mark[p - (up + 1) * C] & 1) && col[p - (up + 1) * C] == x) up++;
+        while (r + dn + 1 < R && !(w.mark[p + (dn + 1) * C] & 1) && col[p + (dn + 1) * C] == x) dn++;
+        if (1 + lft + rgt >= 3) {
+            for (int i = 1; i <= lft; i++) w.mark[p - i] |= 2;
+            for (int i = 1; i <= rgt; i++) w.mark[p + i] |= 2;
+        }
+        if (1 + up + dn >= 3) {
+            for (int i = 1; i <= up; i++) w.mark[p - i * C] |= 2;
+            for (int i = 1; i <= dn; i++) w.mark[p + i * C] |= 2;
+        }
+    }
+    WSYNC();
+    int cleared = 0;
+    for (int p0 = 0; p0 < N; p0 += 64) {
+        int p = p0 + lane;
+        bool clr = p < N && (w.mark[p] & 2);
+        if (clr) { col[p] = 0; typ[p] = 0; }
+        cleared += __popcll(__ballot(clr));
+    }
+    WSYNC();
+    return cleared;
+}
+
+// ------------------------------------------------------------ general (lane 0)
+// Everything below runs on lane 0 only, against LDS.
+template <int MAXN>
+struct Serial {
+    const Params &P;
+    Ws<MAXN> &w;
+    int8_t *col, *typ;
+    int R, C, N;
+    int nl, np;        // lines / pool fill
+    int nm, nmp;       // matches / match-pool fill
+    bool ovf;
+
+    __device__ Serial(const Params &P_, Ws<MAXN> &w_) : P(P_), w(w_) {
+        R = P.R; C = P.C; N = P.N;
+        col = w.brd; typ = w.brd + N;
+        nl = np = nm = nmp = 0;
+        ovf = false;
+    }
+
+    __device__ void clr(int p) {
+        if (col[p] != 0) w.sc[SC_NZ]--;
+        col[p] = 0; typ[p] = 0;
+    }
+
+    // ---- get_colour_lines, board.py:149-215 (rs = bottom-most row with a line)
+    __device__ bool push_line_begin() { return nl < Ws<MAXN>::MLINES; }
+    __device__ void build_lines(int rs) {
+        nl = 0; np = 0;
+        uint64_t hcov = 0;
+        const int row = rs;
+        for (int c = 0; c < C; c++) {
+            int p = row * C + c;
+            if (row > 1 && typ[p] > 0 && col[p] == col[p - C]) {                 // :163-177
+                int start = row - 1;
+                while (start > 0 && col[(start - 1) * C + c] == col[p]) start--;
+                if (row - start >= 2) {
+                    if (nl >= Ws<MAXN>::MLINES || np + (row - start + 1) > Ws<MAXN>::POOL) { ovf = true; return; }
+                    w.ls[nl] = (int16_t)np; w.ll[nl] = (int16_t)(row - start + 1);
+                    for (int i = start; i <= row; i++) w.pool[np++] = (int16_t)(i * C + c);
+                    nl++;
+                }
+            }
+            if (c < C - 2 && !((hcov >> c) & 1) && typ[p] > 0 && col[p] == col[p + 1]) {   // :179-193
+                int end = c + 1;
+                while (end < C - 1 && col[row * C + end + 1] == col[p]) end++;
+                if (end - c >= 2) {
+                    if (nl >= Ws<MAXN>::MLINES || np + (end - c + 1) > Ws<MAXN>::POOL) { ovf = true; return; }
+                    w.ls[nl] = (int16_t)np; w.ll[nl] = (int16_t)(end - c + 1);
+                    for (int i = c; i <= end; i++) { w.pool[np++] = (int16_t)(row * C + i); hcov |= 1ULL << i; }
+                    nl++;
+                }
+            }
+        }
+        // perpendicular pass over the static coord list, :195-214
+        const int ncoords = np;
+        for (int i = 0; i < ncoords; i++) w.mark[w.pool[i]] = 1;
+        // directions (0,1),(1,0),(0,-1),(-1,0): the last two walk the same cells
+        // as the first two, so their sorted lines are always duplicates
+        for (int ci = 0; ci < ncoords && !ovf; ci++) {
+            const int cp = w.pool[ci];
+            const int cr = cp / C, cc = cp - cr * C;
+            for (int d = 0; d < 2; d++) {
+                const int st = np;
+                if (np + R + C + 1 > Ws<MAXN>::POOL || nl >= Ws<MAXN>::MLINES) { ovf = true; break; }
+                w.pool[np++] = (int16_t)cp;
+                for (int s = 0; s < 2; s++) {
+                    int dr = d == 1 ? (s ? -1 : 1) : 0, dc = d == 0 ? (s ? -1 : 1) : 0;
+                    int nr = cr + dr, nc = cc + dc;
+                    while (nr >= 0 && nr < R && nc >= 0 && nc < C) {
+                        int cell = nr * C + nc;
+                        if (w.mark[cell]) break;                                    // n in coords
+                        if (!(col[cp] == col[cell] && typ[cp] > 0 && typ[cell] > 0)) break;   // match_color
+                        w.pool[np++] = (int16_t)cell;
+                        nr += dr; nc += dc;
+                    }
+                }
+                const int len = np - st;
+                if (len >= 3) {
+                    for (int i = st + 1; i < np; i++) {                             // sorted()
+                        int16_t x = w.pool[i]; int j = i - 1;
+                        while (j >= st && w.pool[j] > x) { w.pool[j + 1] = w.pool[j]; j--; }
+                        w.pool[j + 1] = x;
+                    }
+                    bool dup = false;                                               // not in lines
+                    for (int l = 0; l < nl && !dup; l++) {
+                        if (w.ll[l] != len) continue;
+                        bool same = true;
+                        for (int i = 0; i < len; i++) if (w.pool[w.ls[l] + i] != w.pool[st + i]) { same = false; break; }
+                        dup = same;
+                    }
+                    if (dup) np = st;
+                    else { w.ls[nl] = (int16_t)st; w.ll[nl] = (int16_t)len; nl++; }
+                } else {
+                    np = st;
+                }
+            }
+        }
+        for (int i = 0; i < ncoords; i++) w.mark[w.pool[i]] = 0;
+    }
+
+    __device__ bool line_has(int l, int cell) {
+        for (int i = 0; i < w.ll[l]; i++) if (w.pool[w.ls[l] + i] == cell) return true;
+        return false;
+    }
+
+    __device__ int add_match(int name, int colour) {
+        if (nm >= Ws<MAXN>::MM) { ovf = true; return -1; }
+        w.ms[nm] = (int16_t)nmp; w.mlen[nm] = 0; w.mname[nm] = (int8_t)name; w.mcol[nm] = (int8_t)colour;
+        return nm++;
+    }
+    __device__ void match_push(int m, int cell) {
+        if (nmp >= Ws<MAXN>::MPOOL) { ovf = true; return; }
+        w.mpool[nmp++] = (int16_t)cell; w.mlen[m]++;
+    }
+
+    // ---- process_colour_lines, board.py:269-327
+    __device__ void process_lines() {
+        const int S = P.smask;
+        nm = 0; nmp = 0;
+        // lines are already sorted internally; stable sort by first row (:282)
+        int qn = 0;
+        for (int l = 0; l < nl; l++) {
+            int key = w.pool[w.ls[l]] / C, j = qn - 1;
+            while (j >= 0 && w.pool[w.ls[w.q[j]]] / C > key) { w.q[j + 1] = w.q[j]; j--; }
+            w.q[j + 1] = (int16_t)l;
+            qn++;
+        }
+        int head = 0;
+        while (head < qn && !ovf) {
+            const int L = w.q[head++];                                              // pop(0)
+            const int ls = w.ls[L], ln = w.ll[L];
+            if (ln >= 5 && (S & SP_COOKIE)) {                                       // :287-292
+                int m = add_match(M_COOKIE, 0); if (m < 0) return;
+                for (int i = 0; i < 5; i++) match_push(m, w.pool[ls + i]);
+                if (ln - 5 > 2) {
+                    if (nl >= Ws<MAXN>::MLINES || qn >= Ws<MAXN>::MQ) { ovf = true; return; }
+                    w.ls[nl] = (int16_t)(ls + 5); w.ll[nl] = (int16_t)(ln - 5);
+                    w.q[qn++] = (int16_t)nl; nl++;
+                }
+            } else if (ln == 4) {                                                   // :294-302
+                int name;
+                if (w.pool[ls] / C == w.pool[ls + 1] / C && (S & SP_HLASER)) name = M_HLASER;
+                else if (S & SP_VLASER) name = M_VLASER;
+                else name = M_NORMAL;
+                int m = add_match(name, col[w.pool[ls]]); if (m < 0) return;
+                for (int i = 0; i < 4; i++) match_push(m, w.pool[ls + i]);
+            } else {
+                bool shared_any = false;
+                if (S & SP_BOMB)
+                    for (int h = head; h < qn && !shared_any; h++)
+                        for (int i = 0; i < ln; i++) if (line_has(w.q[h], w.pool[ls + i])) { shared_any = true; break; }
+                if (shared_any) {                                                   // :304-320
+                    for (int h = head; h < qn; h++) {
+                        const int O = w.q[h];
+                        int shared = -1;
+                        for (int i = 0; i < ln; i++) if (line_has(O, w.pool[ls + i])) { shared = w.pool[ls + i]; break; }
+                        if (shared < 0) continue;
+                        const int sr = shared / C, scc = shared - sr * C;
+                        const int os = w.ls[O], on = w.ll[O];
+                        // three closest coords of O (stable sort by manhattan distance)
+                        int pick[3], npk = 0;
+                        {
+                            int lastd = -1, lasti = -1;
+                            for (int t = 0; t < 3 && t < on; t++) {
+                                int bd = 1 << 30, bi = -1;
+                                for (int i = 0; i < on; i++) {
+                                    int v = w.pool[os + i];
+                                    int d = abs(v / C - sr) + abs(v % C - scc);
+                                    bool after = d > lastd || (d == lastd && i > lasti);
+                                    if (after && d < bd) { bd = d; bi = i; }
+                                }
+                                pick[npk++] = w.pool[os + bi];
+                                lastd = bd; lasti = bi;
+                            }
+                        }
+                        int m = add_match(M_BOMB, col[w.pool[ls]]); if (m < 0) return;
+                        for (int i = 0; i < ln; i++) match_push(m, w.pool[ls + i]);
+                        for (int t = 0; t < npk; t++) {
+                            bool inl = false;
+                            for (int i = 0; i < ln; i++) if (w.pool[ls + i] == pick[t]) { inl = true; break; }
+                            if (!inl) match_push(m, pick[t]);
+                        }
+                        if (on < 6) {                                               // lines.remove(l)
+                            for (int j = h; j < qn - 1; j++) w.q[j] = w.q[j + 1];
+                            qn--;
+                        } else {                                                    // l.remove(c) in place
+                            for (int t = 0; t < npk; t++) {
+                                int n = w.ll[O];
+                                for (int i = 0; i < n; i++)
+                                    if (w.pool[os + i] == pick[t]) {
+                                        for (int u = i; u < n - 1; u++) w.pool[os + u] = w.pool[os + u + 1];
+                                        w.ll[O] = (int16_t)(n - 1);
+                                        break;
+                                    }
+                            }
+                        }
+                        break;
+                    }
+                } else if (ln >= 3) {                                               // :322-325
+                    int m = add_match(M_NORMAL, col[w.pool[ls]]); if (m < 0) return;
+                    for (int i = 0; i < ln; i++) match_push(m, w.pool[ls + i]);
+                }
+            }
+        }
+    }
+
+    // ---- activate_special, board.py:473-556, as an explicit DFS
+    // frame kinds: 2 v-laser sweep, 3 h-laser sweep, 4 bomb 3x3, -1 cookie scan
+    int sp;
+    __device__ void enter(int cell, int t, bool combo) {
+        if (w.sc[SC_NZ] == 0) return;                        // :488-489 np.all(colour == 0)
+        if (t == 0 || t == 1) { w.sc[SC_ERR] = 1; return; }  // :491-492
+        clr(cell);                                           // :496
+        if (!combo) w.sc[SC_NACT]++;                         // :498-499
+        if (sp >= Ws<MAXN>::MSTK) { ovf = true; return; }
+        if (t == 2 || t == 3 || t == 4) {
+            w.fcell[sp] = (int16_t)cell; w.ftype[sp] = (int8_t)t; w.fidx[sp] = 0; w.faux[sp] = 0; sp++;
+        } else if (t == -1) {                                // :530-545
+            int counts[16];
+            for (int i = 0; i < 16; i++) counts[i] = 0;
+            int any = 0, big = 0;
+            for (int p = 0; p < N; p++) {
+                int v = col[p];
+                if (v != 0) { any = 1; if (v > 0 && v < 16) counts[v]++; else big = 1; }
+            }
+            if (!any) return;
+            if (big) { w.sc[SC_ERR] = 2; return; }
+            int mcc = 0;
+            for (int v = 1; v < 16; v++) if (counts[v] > counts[mcc]) mcc = v;
+            for (int p = 0; p < N; p++) if (col[p] == mcc && typ[p] == 1) clr(p);
+            w.fcell[sp] = (int16_t)cell; w.ftype[sp] = -1; w.fidx[sp] = 0; w.faux[sp] = (int8_t)mcc; sp++;
+        } else {
+            w.sc[SC_ERR] = 3;                                // :555-556
+        }
+    }
+    __device__ void run_dfs() {
+        while (sp > 0 && !ovf && !w.sc[SC_ERR]) {
+            const int f = sp - 1;
+            const int t = w.ftype[f];
+            const int cell = w.fcell[f];
+            const int r = cell / C, c = cell - r * C;
+            int idx = w.fidx[f];
+            int target = -1;
+            if (t == 2) {                                    // :502-507 column sweep
+                if (idx >= R) { sp--; continue; }
+                target = idx * C + c;
+            } else if (t == 3) {                             // :510-515 row sweep
+                if (idx >= C) { sp--; continue; }
+                target = r * C + idx;
+            } else if (t == 4) {                             // :517-528 clipped 3x3
+                int r0 = r > 0 ? r - 1 : 0, r1 = r < R - 1 ? r + 1 : R - 1;
+                int c0 = c > 0 ? c - 1 : 0, c1 = c < C - 1 ? c + 1 : C - 1;
+                int wdt = c1 - c0 + 1;
+                if (idx >= (r1 - r0 + 1) * wdt) { sp--; continue; }
+                target = (r0 + idx / wdt) * C + c0 + idx % wdt;
+            } else {                                         // :546-554 cookie: same-colour specials
+                const int mcc = w.faux[f];
+                while (idx < N && !(typ[idx] > 1 && col[idx] == mcc)) idx++;
+                if (idx >= N) { sp--; continue; }
+                w.fidx[f] = (int16_t)(idx + 1);
+                enter(idx, typ[idx], false);
+                continue;
+            }
+            w.fidx[f] = (int16_t)(idx + 1);
+            int tt = typ[target];
+            if (tt != 0 && tt != 1) enter(target, tt, false);
+            else clr(target);
+        }
+    }
+    __device__ void activate(int cell, int t, bool combo) {
+        sp = 0;
+        enter(cell, t, combo);
+        run_dfs();
+    }
+
+    // ---- get_special_creation_pos, board.py:429-458
+    __device__ int creation_pos(int m, const int16_t *taken, int nt, bool straight) {
+        const int ms = w.ms[m], ml = w.mlen[m];
+        int valid[64]; int nv = 0;
+        for (int i = 0; i < ml; i++) {
+            int v = w.mpool[ms + i]; bool tk = false;
+            for (int j = 0; j < nt; j++) if (taken[j] == v) { tk = true; break; }
+            if (!tk && nv < 64) valid[nv++] = v;
+        }
+        if (!straight) {
+            int br = -1, bc = -1, bnr = -1, bnc = -1;
+            for (int i = 0; i < ml; i++) {
+                int v = w.mpool[ms + i], r = v / C, c = v % C, nr = 0, nc = 0;
+                for (int j = 0; j < ml; j++) { int u = w.mpool[ms + j]; nr += (u / C == r); nc += (u % C == c); }
+                if (nr > bnr) { bnr = nr; br = r; }
+                if (nc > bnc) { bnc = nc; bc = c; }
+            }
+            int corner = br * C + bc;
+            for (int i = 0; i < nv; i++) if (valid[i] == corner) return corner;
+            if (nv == 0) { w.sc[SC_ERR] = 4; return w.mpool[ms]; }
+            int best = 0, bd = 1 << 30;
+            for (int i = 0; i < nv; i++) {
+                int dr = valid[i] / C - br, dc = valid[i] % C - bc, d = dr * dr + dc * dc;
+                if (d < bd) { bd = d; best = i; }
+            }
+            return valid[best];
+        }
+        if (nv == 0) { w.sc[SC_ERR] = 4; return w.mpool[ms]; }
+        for (int i = 1; i < nv; i++) {
+            int x = valid[i], j = i - 1;
+            while (j >= 0 && valid[j] > x) { valid[j + 1] = valid[j]; j--; }
+            valid[j + 1] = x;
+        }
+        return (nv % 2 == 0) ? valid[nv / 2 - 1] : valid[nv / 2];
+    }
+
+    // ---- resolve_colour_matches, board.py:397-427 (+ resolve_colour_match :460-471, create_special :572-597)
+    __device__ void resolve() {
+        int16_t taken[64]; int nt = 0;
+        int qpos[64], qname[64], qcol[64], nq = 0;
+        for (int m = 0; m < nm; m++) {
+            if (w.mname[m] == M_NORMAL) continue;
+            if (nq >= 64) { ovf = true; return; }
+            int pos = creation_pos(m, taken, nt, w.mname[m] != M_BOMB);
+            bool dup = false;
+            for (int j = 0; j < nt; j++) if (taken[j] == pos) dup = true;
+            if (!dup && nt < 64) taken[nt++] = (int16_t)pos;
+            qpos[nq] = pos; qname[nq] = w.mname[m]; qcol[nq] = w.mcol[m]; nq++;
+        }
+        for (int m = 0; m < nm && !ovf && !w.sc[SC_ERR]; m++) {
+            const int ms = w.ms[m], ml = w.mlen[m];
+            for (int i = 0; i < ml; i++) {
+                int p = w.mpool[ms + i], t = typ[p];
+                if (t != 0 && t != 1) activate(p, t, false);
+                else clr(p);
+            }
+        }
+        const int8_t TT[5] = {0, 2, 3, 4, -1};
+        for (int i = 0; i < nq; i++) {
+            w.sc[SC_NNEW]++;
+            int p = qpos[i];
+            if (col[p] == 0 && qcol[i] != 0) w.sc[SC_NZ]++;
+            else if (col[p] != 0 && qcol[i] == 0) w.sc[SC_NZ]--;
+            col[p] = (int8_t)qcol[i];
+            typ[p] = TT[qname[i]];
+        }
+    }
+
+    // ---- combination_match, board.py:600-719
+    __device__ void combination(int p1, int p2) {
+        w.sc[SC_NACT] += 2;                                                 // :609
+        int t1 = typ[p1], k1 = col[p1], t2 = typ[p2], k2 = col[p2];
+        int r1 = p1 / C, c1 = p1 % C, r2 = p2 / C, c2 = p2 % C;
+        if (t1 == -1 && t2 == -1) {                                         // :615-616
+            for (int p = 0; p < N; p++) { col[p] = 0; typ[p] = 0; }
+            w.sc[SC_NZ] = 0;
+        } else if ((t1 == -1 && t2 == 1) || (t1 == 1 && t2 == -1)) {        // :619-641
+            if (t1 == 1) { int x = p1; p1 = p2; p2 = x; x = k1; k1 = k2; k2 = x; x = t1; t1 = t2; t2 = x; }
+            clr(p1);
+            for (int p = 0; p < N; p++) {                                   // colour_mask & normal_mask
+                w.mark[p] = (col[p] == k2);
+                if (w.mark[p] && typ[p] == 1) clr(p);
+            }
+            for (int p = 0; p < N; p++) w.mark[p] = w.mark[p] && typ[p] > 1;
+            for (int p = 0; p < N && !ovf; p++) {                           // activate_specials_in_mask
+                if (!w.mark[p]) continue;
+                int t = typ[p];
+                if (t != 0 && t != 1) activate(p, t, true);
+            }
+            for (int p = 0; p < N; p++) w.mark[p] = 0;
+            w.sc[SC_NACT] -= 1;
+        } else if ((t1 == -1 && t2 >= 2) || (t1 >= 2 && t2 == -1)) {        // :644-660
+            if (t2 == -1) { int x = p1; p1 = p2; p2 = x; x = k1; k1 = k2; k2 = x; x = t1; t1 = t2; t2 = x; }
+            clr(p1);
+            for (int p = 0; p < N; p++) {
+                w.mark[p] = (col[p] == k2);
+                if (w.mark[p] && typ[p] == 1) typ[p] = (int8_t)t2;
+            }
+            for (int p = 0; p < N && !ovf; p++) {
+                if (!w.mark[p]) continue;
+                int t = typ[p];
+                if (t != 0 && t != 1) activate(p, t, true);
+            }
+            for (int p = 0; p < N; p++) w.mark[p] = 0;
+        } else if ((t1 == 2 || t1 == 3) && (t2 == 2 || t2 == 3)) {          // :663-674
+            clr(p1); clr(p2);
+            int r = r1 < r2 ? r1 : r2, c = c1 < c2 ? c1 : c2;
+            activate(r * C + c, 2, true);
+            activate(r * C + c, 3, true);
+        } else if ((t1 == 4 && t2 >= 2 && t2 <= 3) || (t2 == 4 && t1 >= 2 && t1 <= 3)) {   // :677-696
+            clr(p1); clr(p2);
+            int r = r1 < r2 ? r1 : r2, c = c1 < c2 ? c1 : c2;
+            int a0 = r > 0 ? r - 1 : 0, a1 = r < R - 1 ? r + 1 : R - 1;
+            int b0 = c > 0 ? c - 1 : 0, b1 = c < C - 1 ? c + 1 : C - 1;
+            for (int i = a0; i <= a1; i++) activate(i * C + c, 3, true);
+            for (int j = b0; j <= b1; j++) activate(r * C + j, 2, true);
+        } else if (t1 == 4 && t2 == 4) {                                    // :699-719
+            clr(p1); clr(p2);
+            int r = r1 < r2 ? r1 : r2, c = c1 < c2 ? c1 : c2;
+            int a0 = r > 1 ? r - 2 : 0, a1 = r < R - 2 ? r + 2 : R - 1;
+            int b0 = c > 1 ? c - 2 : 0, b1 = c < C - 2 ? c + 2 : C - 1;
+            for (int i = a0; i <= a1; i++)
+                for (int j = b0; j <= b1; j++) {
+                    int p = i * C + j, t = typ[p];
+                    if (t == 1) clr(p);
+                    else if (t != 0) activate(p, t, true);
+                }
+        }
+    }
+};
+
+// ------------------------------------------------------------------ move()
+// Board.move, board.py:330-395 (the effectiveness test :352 is done by the caller).
+// Returns eliminations; updates the LDS scalars / flags.  Leaves the
+// effective mask of the final board in w.effw.
+template <int MAXN>
+__device__ int board_move(const Params &P, Ws<MAXN> &w, int lane, const LaneJump &J, int p1, int p2,
+                          int &flags) {
+    const int N = P.N;
+    int8_t *col = w.brd, *typ = w.brd + N;
+    int elim = 0;
+    if (lane == 0) {                                                        // swap_coords :355
+        int8_t x = col[p1]; col[p1] = col[p2]; col[p2] = x;
+        x = typ[p1]; typ[p1] = typ[p2]; typ[p2] = x;
+        w.sc[SC_NACT] = 0; w.sc[SC_NNEW] = 0; w.sc[SC_ERR] = 0;
+    }
+    WSYNC();
+    const int t1 = typ[p1], t2 = typ[p2];
+    bool ovf = false;
+    if (((t1 != 0 && t1 != 1) && (t2 != 0 && t2 != 1)) || t1 < 0 || t2 < 0) {   // :357-364
+        flags |= FL_COMBO;
+        int nz = count_colour_nonzero(P, w, lane);
+        if (lane == 0) {
+            w.sc[SC_NZ] = nz;
+            Serial<MAXN> S(P, w);
+            S.combination(p1, p2);
+            w.sc[SC_A] = S.ovf;
+        }
+        WSYNC();
+        ovf |= w.sc[SC_A] != 0;
+        elim += count_type_zero(P, w, lane);
+        gravity(P, w, lane);
+        refill(P, w, lane, J);
+    }
+    // fast path only when no special can exist on the board
+    bool all_normal = true;
+    for (int p = lane; p < N; p += 64) all_normal &= typ[p] == 1;
+    const bool fast = P.smask == 0 && __ballot(!all_normal) == 0ULL;
+    for (;;) {
+        if (ovf) break;                                          // :367-376
+        if (w.sc[SC_ERR]) break;
+        const int rs = detect_row(P, w, lane);
+        if (rs < 0) break;
+        if (fast) {
+            elim += fast_clear(P, w, lane, rs);
+        } else {
+            int nz = count_colour_nonzero(P, w, lane);
+            if (lane == 0) {
+                w.sc[SC_NZ] = nz;
+                Serial<MAXN> S(P, w);
+                S.build_lines(rs);
+                if (!S.ovf) S.process_lines();
+                if (!S.ovf) S.resolve();
+                w.sc[SC_A] = S.ovf;
+            }
+            WSYNC();
+            ovf |= w.sc[SC_A] != 0;
+            elim += count_type_zero(P, w, lane);
+        }
+        gravity(P, w, lane);
+        refill(P, w, lane, J);
+    }
+    elim += w.sc[SC_NNEW];                                                  // :378
+    if (ovf) flags |= FL_OVF;
+    if (w.sc[SC_ERR]) flags |= FL_ERR;
+    if (ensure_playable(P, w, lane, J)) flags |= FL_SHUF;                   // :381-391
+    return elim;
+}
+
+// ------------------------------------------------------------------ kernels
+__device__ inline LaneJump load_jump(const Params &P, int lane) {
+    const uint64_t *t = P.jump + lane * 4;
+    LaneJump J;
+    J.Aj = U128{t[0], t[1]};
+    J.Gj = U128{t[2], t[3]};
+    return J;
+}
+
+template <int MAXN>
+__global__ __launch_bounds__(64 * TMG_WPB) void step_kernel(
+    Params P, int64_t n, int8_t *__restrict__ board, uint64_t *__restrict__ rng, int32_t *__restrict__ timer,
+    const int32_t *__restrict__ actions, int32_t *__restrict__ reward, int32_t *__restrict__ n_new,
+    int32_t *__restrict__ n_act, uint8_t *__restrict__ flags_out, uint64_t *__restrict__ eff, int trust_eff,
+    int autoreset) {
+    extern __shared__ __align__(16) unsigned char smem[];
+    const int lane = threadIdx.x & 63;
+    const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    Ws<MAXN> &w = reinterpret_cast<Ws<MAXN> *>(smem)[wv];
+    const int64_t e = (int64_t)blockIdx.x * TMG_WPB + wv;
+    if (e >= n) return;
+
+    const int N = P.N, W = P.W;
+    const int a = actions[e];
+    const int t0 = timer[e];
+    if (t0 >= P.num_moves || a < 0 || a >= P.A) {                           // tile_match_env.py:94-95
+        if (lane == 0) { reward[e] = 0; n_new[e] = 0; n_act[e] = 0; flags_out[e] = FL_ERR; }
+        return;
+    }
+    int8_t *gb = board + e * 2 * N;
+    uint64_t *ge = eff + e * W;
+    int r1, c1, r2, c2;
+    action_coords(P.R, P.C, a, r1, c1, r2, c2);
+    const int p1 = r1 * P.C + c1, p2 = r2 * P.C + c2;
+
+    load_board(P, w, lane, gb);
+    for (int p = lane; p < N; p += 64) w.mark[p] = 0;
+    WSYNC();
+    bool effective;
+    if (trust_eff) {
+        effective = (ge[a >> 6] >> (a & 63)) & 1ULL;                        // board.py:352 via cached mask
+    } else {
+        bool ex = lane == 0 ? eff_exact(P, w, a) : false;
+        effective = __ballot(ex) != 0ULL;
+    }
+    const int t1 = t0 + 1;
+    const bool done = t1 == P.num_moves;                                    // tile_match_env.py:100-101
+    int flags = done ? FL_DONE : 0;
+    int elim = 0, nn = 0, na = 0;
+    const LaneJump J = load_jump(P, lane);
+    bool changed = false;
+    if (lane < 5) w.rng[lane] = rng[e * 5 + lane];
+    WSYNC();
+    if (effective) {
+        elim = board_move(P, w, lane, J, p1, p2, flags);
+        nn = w.sc[SC_NNEW];
+        na = w.sc[SC_NACT];
+        changed = true;
+    }
+    int tnew = t1;
+    if (done && autoreset) {                                                // reset() without a seed
+        generate_board(P, w, lane, J);
+        tnew = 0;
+        flags |= FL_RESET;
+        changed = true;
+    }
+    if (changed) {
+        store_board(P, w, lane, gb);
+        if (lane < 5) rng[e * 5 + lane] = w.rng[lane];
+    }
+    if (done && !autoreset) {
+        for (int i = lane; i < W; i += 64) ge[i] = 0ULL;                   // tile_match_env.py:119-120
+    } else if (changed) {
+        for (int i = lane; i < W; i += 64) ge[i] = w.effw[i];
+    } else if (!trust_eff) {
+        scan_effective(P, w, lane);
+        for (int i = lane; i < W; i += 64) ge[i] = w.effw[i];
+    }
+    if (lane == 0) {
+        timer[e] = tnew;
+        reward[e] = elim;
+        n_new[e] = nn;
+        n_act[e] = na;
+        flags_out[e] = (uint8_t)flags;
+    }
+}
+
+template <int MAXN>
+__global__ __launch_bounds__(64 * TMG_WPB) void reset_kernel(Params P, int64_t n, int8_t *__restrict__ board,
+                                                             uint64_t *__restrict__ rng, int32_t *__restrict__ timer,
+                                                             uint64_t *__restrict__ eff,
+                                                             const uint8_t *__restrict__ env_mask) {
+    extern __shared__ __align__(16) unsigned char smem[];
+    const int lane = threadIdx.x & 63;
+    const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    Ws<MAXN> &w = reinterpret_cast<Ws<MAXN> *>(smem)[wv];
+    const int64_t e = (int64_t)blockIdx.x * TMG_WPB + wv;
+    if (e >= n) return;
+    if (env_mask && !env_mask[e]) return;
+    const int N = P.N, W = P.W;
+    const LaneJump J = load_jump(P, lane);
+    if (lane < 5) w.rng[lane] = rng[e * 5 + lane];
+    WSYNC();
+    generate_board(P, w, lane, J);                                          // board.py:95-109
+    store_board(P, w, lane, board + e * 2 * N);
+    if (lane < 5) rng[e * 5 + lane] = w.rng[lane];
+    for (int i = lane; i < W; i += 64) eff[e * W + i] = w.effw[i];
+    if (lane == 0) timer[e] = 0;
+}
+
+template <int MAXN>
+__global__ __launch_bounds__(64 * TMG_WPB) void effective_kernel(Params P, int64_t n, const int8_t *__restrict__ board,
+                                                                 uint64_t *__restrict__ eff) {
+    extern __shared__ __align__(16) unsigned char smem[];
+    const int lane = threadIdx.x & 63;
+    const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    Ws<MAXN> &w = reinterpret_cast<Ws<MAXN> *>(smem)[wv];
+    const int64_t e = (int64_t)blockIdx.x * TMG_WPB + wv;
+    if (e >= n) return;
+    load_board(P, w, lane, board + e * 2 * P.N);
+    WSYNC();
+    scan_effective(P, w, lane);
+    for (int i = lane; i < P.W; i += 64) eff[e * P.W + i] = w.effw[i];
+}
+
+}  // namespace tmg

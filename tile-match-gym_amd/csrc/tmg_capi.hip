@@ -1,0 +1,147 @@
+// tmg_capi.hip — extern "C" entry points of libtmg.so (declared in include/tmg.h).
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstring>
+#include <string>
+
+#include "tmg.h"
+#include "tmg_board.hip"
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const std::string &msg) {
+    g_err = msg;
+    return code;
+}
+
+int hip_check(hipError_t e, const char *what) {
+    if (e != hipSuccess) return fail(-5, std::string(what) + ": " + hipGetErrorString(e));
+    return 0;
+}
+
+}  // namespace
+
+struct tmg_ctx {
+    int device;
+    tmg::Params P;
+    uint64_t *d_jump;
+    int maxn;
+};
+
+using tmg::Params;
+
+template <int MAXN>
+static int launch_all(int which, tmg_ctx *ctx, int64_t n, int8_t *board, uint64_t *rng, int32_t *timer,
+                      const int32_t *actions, int32_t *reward, int32_t *n_new, int32_t *n_act, uint8_t *flags,
+                      uint64_t *eff, const uint8_t *env_mask, int trust_eff, int autoreset, hipStream_t s) {
+    const size_t lds = sizeof(tmg::Ws<MAXN>) * TMG_WPB;
+    const dim3 block(64 * TMG_WPB);
+    const dim3 grid((unsigned)((n + TMG_WPB - 1) / TMG_WPB));
+    if (which == 0)
+        hipLaunchKernelGGL(tmg::step_kernel<MAXN>, grid, block, lds, s, ctx->P, n, board, rng, timer, actions, reward,
+                           n_new, n_act, flags, eff, trust_eff, autoreset);
+    else if (which == 1)
+        hipLaunchKernelGGL(tmg::reset_kernel<MAXN>, grid, block, lds, s, ctx->P, n, board, rng, timer, eff, env_mask);
+    else
+        hipLaunchKernelGGL(tmg::effective_kernel<MAXN>, grid, block, lds, s, ctx->P, n, (const int8_t *)board, eff);
+    return hip_check(hipGetLastError(), "kernel launch");
+}
+
+static int dispatch(int which, tmg_ctx *ctx, int64_t n, int8_t *board, uint64_t *rng, int32_t *timer,
+                    const int32_t *actions, int32_t *reward, int32_t *n_new, int32_t *n_act, uint8_t *flags,
+                    uint64_t *eff, const uint8_t *env_mask, int trust_eff, int autoreset, void *stream) {
+    if (!ctx) return fail(-1, "null context");
+    if (n < 0) return fail(-2, "negative batch size");
+    if (n == 0) return 0;
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    if (dev != ctx->device) {
+        int rc = hip_check(hipSetDevice(ctx->device), "hipSetDevice");
+        if (rc) return rc;
+    }
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    if (ctx->maxn == 128)
+        return launch_all<128>(which, ctx, n, board, rng, timer, actions, reward, n_new, n_act, flags, eff, env_mask,
+                               trust_eff, autoreset, s);
+    return launch_all<512>(which, ctx, n, board, rng, timer, actions, reward, n_new, n_act, flags, eff, env_mask,
+                           trust_eff, autoreset, s);
+}
+
+extern "C" {
+
+int tmg_create(tmg_ctx **out, int device, int rows, int cols, int colours, uint32_t specials_mask, int num_moves) {
+    if (!out) return fail(-1, "null output pointer");
+    *out = nullptr;
+    if (rows < 2 || cols < 2) return fail(-2, "board must be at least 2x2");
+    if (rows > 64 || cols > 64 || rows * cols > 512) return fail(-2, "board too large (R,C <= 64, R*C <= 512)");
+    if (colours < 1 || colours > 15) return fail(-2, "num_colours must be in [1, 15]");
+    if (specials_mask > 15u) return fail(-2, "bad specials mask");
+    if (num_moves < 1) return fail(-2, "num_moves must be >= 1");
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return fail(-3, "no HIP device available");
+    if (device < 0 || device >= ndev) return fail(-3, "bad device index");
+    int rc = hip_check(hipSetDevice(device), "hipSetDevice");
+    if (rc) return rc;
+    tmg_ctx *c = new tmg_ctx();
+    c->device = device;
+    Params &P = c->P;
+    P.R = rows; P.C = cols; P.N = rows * cols;
+    P.A = 2 * rows * cols - rows - cols;
+    P.W = (P.A + 63) / 64;
+    P.k = colours;
+    P.smask = (int)specials_mask;
+    P.num_moves = num_moves;
+    {
+        uint32_t rng = (uint32_t)(colours - 1), excl = rng + 1;
+        P.thr = rng ? (UINT32_MAX - rng) % excl : 0u;
+    }
+    c->maxn = P.N <= 128 ? 128 : 512;
+    uint64_t tab[64 * 4];
+    tmg::build_jump_table(tab);
+    rc = hip_check(hipMalloc(&c->d_jump, sizeof tab), "hipMalloc");
+    if (rc) { delete c; return rc; }
+    rc = hip_check(hipMemcpy(c->d_jump, tab, sizeof tab, hipMemcpyHostToDevice), "hipMemcpy");
+    if (rc) { (void)hipFree(c->d_jump); delete c; return rc; }
+    P.jump = c->d_jump;
+    *out = c;
+    return 0;
+}
+
+int tmg_destroy(tmg_ctx *ctx) {
+    if (!ctx) return 0;
+    (void)hipFree(ctx->d_jump);
+    delete ctx;
+    return 0;
+}
+
+int tmg_reset(tmg_ctx *ctx, int64_t n, int8_t *board, uint64_t *rng, int32_t *timer, uint64_t *eff,
+              const uint8_t *env_mask, void *stream) {
+    if (!board || !rng || !timer || !eff) return fail(-1, "null state buffer");
+    return dispatch(1, ctx, n, board, rng, timer, nullptr, nullptr, nullptr, nullptr, nullptr, eff, env_mask, 0, 0,
+                    stream);
+}
+
+int tmg_step(tmg_ctx *ctx, int64_t n, int8_t *board, uint64_t *rng, int32_t *timer, const int32_t *actions,
+             int32_t *reward, int32_t *n_new, int32_t *n_act, uint8_t *flags, uint64_t *eff, int trust_eff,
+             int autoreset, void *stream) {
+    if (!board || !rng || !timer || !actions || !reward || !n_new || !n_act || !flags || !eff)
+        return fail(-1, "null buffer");
+    return dispatch(0, ctx, n, board, rng, timer, actions, reward, n_new, n_act, flags, eff, nullptr, trust_eff,
+                    autoreset, stream);
+}
+
+int tmg_effective(tmg_ctx *ctx, int64_t n, const int8_t *board, uint64_t *eff, void *stream) {
+    if (!board || !eff) return fail(-1, "null buffer");
+    return dispatch(2, ctx, n, const_cast<int8_t *>(board), nullptr, nullptr, nullptr, nullptr, nullptr, nullptr,
+                    nullptr, eff, nullptr, 0, 0, stream);
+}
+
+int tmg_num_actions(const tmg_ctx *ctx) { return ctx ? ctx->P.A : -1; }
+int tmg_mask_words(const tmg_ctx *ctx) { return ctx ? ctx->P.W : -1; }
+const char *tmg_last_error(void) { return g_err.c_str(); }
+int tmg_abi_version(void) { return 1; }
+
+}  // extern "C"

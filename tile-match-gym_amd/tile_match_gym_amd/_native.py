@@ -1,0 +1,111 @@
+"""ctypes binding of libtmg.so (include/tmg.h).
+
+This is the reference-side binding a maintainer would add: the reference has
+no FFI, so the binding replaces the Python Board calls of
+tile_match_env.py:49-124 with the C entry points below.  There is no CPU
+fallback: if the library or a HIP device is missing, every call raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "_lib", "libtmg.so")
+EXPORTS = ("tmg_create", "tmg_destroy", "tmg_reset", "tmg_step", "tmg_effective",
+           "tmg_num_actions", "tmg_mask_words", "tmg_last_error", "tmg_abi_version")
+ABI_VERSION = 1
+
+SPECIAL_BITS = {"cookie": 1, "vertical_laser": 2, "horizontal_laser": 4, "bomb": 8}
+FLAG_DONE, FLAG_COMBO, FLAG_SHUFFLED, FLAG_RESET, FLAG_OVERFLOW, FLAG_ERROR = 1, 2, 4, 8, 0x40, 0x80
+
+_lib = None
+
+P = ctypes.c_void_p
+I = ctypes.c_int
+I64 = ctypes.c_int64
+
+
+class TmgError(RuntimeError):
+    pass
+
+
+def load():
+    """Load libtmg.so (raises TmgError when it was not built)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise TmgError(f"{LIB_PATH} not found: build it with `make -C tile-match-gym_amd` "
+                       "(or __graft_entry__.build()); there is no CPU fallback")
+    L = ctypes.CDLL(LIB_PATH)
+    L.tmg_create.argtypes = [ctypes.POINTER(P), I, I, I, I, ctypes.c_uint32, I]
+    L.tmg_destroy.argtypes = [P]
+    L.tmg_reset.argtypes = [P, I64, P, P, P, P, P, P]
+    L.tmg_step.argtypes = [P, I64, P, P, P, P, P, P, P, P, P, I, I, P]
+    L.tmg_effective.argtypes = [P, I64, P, P, P]
+    L.tmg_num_actions.argtypes = [P]
+    L.tmg_mask_words.argtypes = [P]
+    L.tmg_last_error.argtypes = []
+    L.tmg_last_error.restype = ctypes.c_char_p
+    L.tmg_abi_version.argtypes = []
+    for name in ("tmg_create", "tmg_destroy", "tmg_reset", "tmg_step", "tmg_effective",
+                 "tmg_num_actions", "tmg_mask_words", "tmg_abi_version"):
+        getattr(L, name).restype = I
+    if L.tmg_abi_version() != ABI_VERSION:
+        raise TmgError("libtmg.so ABI version mismatch; rebuild it")
+    _lib = L
+    return L
+
+
+def check(rc: int):
+    if rc != 0:
+        msg = load().tmg_last_error().decode(errors="replace")
+        raise TmgError(f"libtmg error {rc}: {msg}")
+
+
+def specials_mask(colourless_specials, colour_specials) -> int:
+    m = 0
+    for name in list(colourless_specials) + list(colour_specials):
+        if name not in SPECIAL_BITS:
+            raise ValueError(f"unknown special {name!r}")
+        m |= SPECIAL_BITS[name]
+    return m
+
+
+class Context:
+    """Owns a tmg_ctx (shape / colours / specials / episode length on one device)."""
+
+    def __init__(self, device_index: int, rows: int, cols: int, colours: int, smask: int, num_moves: int):
+        L = load()
+        h = P()
+        check(L.tmg_create(ctypes.byref(h), int(device_index), int(rows), int(cols), int(colours),
+                           int(smask), int(num_moves)))
+        self._h = h
+        self.num_actions = L.tmg_num_actions(h)
+        self.mask_words = L.tmg_mask_words(h)
+
+    @property
+    def handle(self):
+        return self._h
+
+    def close(self):
+        if getattr(self, "_h", None) is not None and self._h.value:
+            load().tmg_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def reset(self, n, board, rng, timer, eff, env_mask, stream):
+        check(load().tmg_reset(self._h, int(n), board, rng, timer, eff, env_mask, stream))
+
+    def step(self, n, board, rng, timer, actions, reward, n_new, n_act, flags, eff, trust_eff, autoreset, stream):
+        check(load().tmg_step(self._h, int(n), board, rng, timer, actions, reward, n_new, n_act, flags, eff,
+                              int(trust_eff), int(autoreset), stream))
+
+    def effective(self, n, board, eff, stream):
+        check(load().tmg_effective(self._h, int(n), board, eff, stream))

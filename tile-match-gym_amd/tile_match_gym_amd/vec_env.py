@@ -1,0 +1,129 @@
+"""TileMatchVecEnv — N independent TileMatchEnv boards stepped by one HIP launch.
+
+State lives in PyTorch-ROCm tensors on one device (layout: include/tmg.h);
+each reset/step enqueues one kernel on the current torch stream through the
+C ABI.  Per env the semantics are the reference's TileMatchEnv
+(tile_match_env.py:84-124) with one numpy PCG64 stream per env, so env i
+seeded with s follows exactly the trajectory of TileMatchEnv(..., seed=s).
+
+Autoreset (default on): an env whose episode ends is regenerated inside the
+same step call, continuing its RNG stream (== the reference's reset() without
+a seed, tile_match_env.py:84-87); reward/flags describe the final move,
+`info["final_board"]` is not kept (pass autoreset=False to inspect it).
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+
+from . import _native
+from .seeding import batch_rng_words, rng_words_from_seed
+
+
+def _ptr(t: torch.Tensor):
+    return t.data_ptr() if t is not None else None
+
+
+class TileMatchVecEnv:
+    def __init__(self, num_envs: int, num_rows: int, num_cols: int, num_colours: int, num_moves: int,
+                 colourless_specials=(), colour_specials=(), seed: int = 0, seeds=None, device=None,
+                 autoreset: bool = True):
+        if device is None:
+            device = torch.device("cuda", torch.cuda.current_device())
+        device = torch.device(device)
+        if device.type != "cuda":
+            raise _native.TmgError("TileMatchVecEnv runs on a HIP device only (no CPU fallback)")
+        self.device = device
+        self.num_envs = int(num_envs)
+        self.num_rows, self.num_cols, self.num_colours, self.num_moves = num_rows, num_cols, num_colours, num_moves
+        self.colourless_specials = list(colourless_specials)
+        self.colour_specials = list(colour_specials)
+        self.specials_mask = _native.specials_mask(colourless_specials, colour_specials)
+        self.autoreset = bool(autoreset)
+        self.ctx = _native.Context(device.index if device.index is not None else torch.cuda.current_device(),
+                                   num_rows, num_cols, num_colours, self.specials_mask, num_moves)
+        self.num_actions = self.ctx.num_actions
+        self.mask_words = self.ctx.mask_words
+        N = self.num_envs
+        kw = dict(device=device)
+        self.board = torch.zeros((N, 2, num_rows, num_cols), dtype=torch.int8, **kw)
+        if seeds is None:
+            seeds = range(int(seed), int(seed) + N)
+        self.rng = torch.from_numpy(batch_rng_words(seeds).view(np.int64)).to(device)
+        self.timer = torch.zeros(N, dtype=torch.int32, **kw)
+        self.eff = torch.zeros((N, self.mask_words), dtype=torch.int64, **kw)
+        self.reward = torch.zeros(N, dtype=torch.int32, **kw)
+        self.n_new = torch.zeros(N, dtype=torch.int32, **kw)
+        self.n_act = torch.zeros(N, dtype=torch.int32, **kw)
+        self.flags = torch.zeros(N, dtype=torch.uint8, **kw)
+        self._eff_valid = False
+
+    # ----------------------------------------------------------------- API
+    def _stream(self):
+        return torch.cuda.current_stream(self.device).cuda_stream
+
+    def set_seed(self, seeds):
+        """Re-seed every env (== tile_match_env.py:79-82 per env)."""
+        w = batch_rng_words(seeds)
+        self.rng.copy_(torch.from_numpy(w.view(np.int64)))
+
+    def reset(self, seed=None, env_mask=None):
+        if seed is not None:
+            self.set_seed(range(int(seed), int(seed) + self.num_envs))
+        m = None
+        if env_mask is not None:
+            m = torch.as_tensor(env_mask, device=self.device).to(torch.uint8).contiguous()
+        self.ctx.reset(self.num_envs, _ptr(self.board), _ptr(self.rng), _ptr(self.timer), _ptr(self.eff),
+                       _ptr(m), self._stream())
+        self._eff_valid = True
+        return self._obs(), {"effective_bits": self.eff}
+
+    def step(self, actions):
+        a = torch.as_tensor(actions, device=self.device)
+        if a.dtype != torch.int32:
+            a = a.to(torch.int32)
+        a = a.contiguous()
+        if a.shape != (self.num_envs,):
+            raise ValueError(f"actions must have shape ({self.num_envs},)")
+        self.step_raw(a)
+        flags = self.flags
+        info = {
+            "is_combination_match": (flags & _native.FLAG_COMBO) != 0,
+            "num_new_specials": self.n_new,
+            "num_specials_activated": self.n_act,
+            "shuffled": (flags & _native.FLAG_SHUFFLED) != 0,
+            "effective_bits": self.eff,
+            "error": (flags & _native.FLAG_ERROR) != 0,
+        }
+        done = (flags & _native.FLAG_DONE) != 0
+        return self._obs(), self.reward, done, torch.zeros_like(done), info
+
+    def step_raw(self, actions_i32: torch.Tensor):
+        """Enqueue one batched step (no output post-processing): the bench path."""
+        self.ctx.step(self.num_envs, _ptr(self.board), _ptr(self.rng), _ptr(self.timer), _ptr(actions_i32),
+                      _ptr(self.reward), _ptr(self.n_new), _ptr(self.n_act), _ptr(self.flags), _ptr(self.eff),
+                      int(self._eff_valid), int(self.autoreset), self._stream())
+        self._eff_valid = True
+
+    def invalidate_effective_cache(self):
+        """Call after editing self.board by hand."""
+        self._eff_valid = False
+
+    def compute_effective(self):
+        self.ctx.effective(self.num_envs, _ptr(self.board), _ptr(self.eff), self._stream())
+        return self.eff
+
+    def effective_mask(self) -> torch.Tensor:
+        """(N, A) bool mask of effective actions, unpacked from the bitmask."""
+        bits = torch.arange(64, device=self.device, dtype=torch.int64)
+        m = ((self.eff.unsqueeze(-1) >> bits) & 1).reshape(self.num_envs, -1)[:, :self.num_actions]
+        return m.bool()
+
+    def _obs(self):
+        return {"board": self.board, "num_moves_left": self.num_moves - self.timer}
+
+    def rng_words(self) -> np.ndarray:
+        return self.rng.cpu().numpy().view(np.uint64)
+
+    def close(self):
+        self.ctx.close()
