@@ -1,0 +1,53 @@
+"""CPU-side check of the HIP kernel *logic*: tools/wave_emu compiles
+csrc/tmg_board.hip for the host (one fiber per lane, collectives resolved at
+the wavefront's lockstep points) and replays the reference's golden
+trajectories through it.  This is a debugging aid that runs without a GPU;
+the parity gate proper is tests/test_gpu_parity.py on the MI355X."""
+import os
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+from golden_io import load_traj, traj_names, replay_trajectory
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+EMU_DIR = os.path.join(ROOT, "tools", "wave_emu")
+
+
+@pytest.fixture(scope="module")
+def emu_lib():
+    asan = os.environ.get("TMG_EMU_ASAN") == "1"
+    subprocess.run(["make", "-C", EMU_DIR, "libwave_emu_asan.so" if asan else "libwave_emu.so"], check=True,
+                   stdout=subprocess.DEVNULL)
+    sys.path.insert(0, EMU_DIR)
+    import emu
+    return emu, emu.load(asan=asan)
+
+
+class _EmuBackend:
+    def __init__(self, emu, L, d):
+        self.b = emu.EmuBatch(L, d["R"], d["C"], d["k"], d["smask"], d["num_moves"], d["init_rng"])
+
+    def reset(self):
+        self.b.reset()
+
+    def step(self, a, autoreset):
+        self.b.step(a, autoreset)
+
+    get_board = lambda self: self.b.board
+    get_rng = lambda self: self.b.rng
+    get_eff = lambda self: self.b.eff
+    get_reward = lambda self: self.b.reward
+    get_flags = lambda self: self.b.flags
+    get_n_new = lambda self: self.b.n_new
+    get_n_act = lambda self: self.b.n_act
+
+
+@pytest.mark.parametrize("name", traj_names())
+@pytest.mark.parametrize("autoreset", [False, True])
+def test_trajectory_golden_emulated(emu_lib, name, autoreset):
+    emu, L = emu_lib
+    d = load_traj(name)
+    assert replay_trajectory(d, _EmuBackend(emu, L, d), autoreset) > 0

@@ -20,7 +20,7 @@ struct U128 {
     uint64_t lo, hi;
 };
 
-__host__ __device__ inline U128 mul128(U128 a, U128 b) {   // low 128 bits of a*b
+__host__ __device__ __forceinline__ U128 mul128(U128 a, U128 b) {   // low 128 bits of a*b
 #if defined(__HIP_DEVICE_COMPILE__)
     uint64_t hi = __umul64hi(a.lo, b.lo) + a.lo * b.hi + a.hi * b.lo;
 #else
@@ -29,14 +29,14 @@ __host__ __device__ inline U128 mul128(U128 a, U128 b) {   // low 128 bits of a*
     return U128{a.lo * b.lo, hi};
 }
 
-__host__ __device__ inline U128 add128(U128 a, U128 b) {
+__host__ __device__ __forceinline__ U128 add128(U128 a, U128 b) {
     U128 r;
     r.lo = a.lo + b.lo;
     r.hi = a.hi + b.hi + (r.lo < a.lo ? 1 : 0);
     return r;
 }
 
-__host__ __device__ inline uint64_t xsl_rr(U128 s) {
+__host__ __device__ __forceinline__ uint64_t xsl_rr(U128 s) {
     uint64_t x = s.hi ^ s.lo;
     unsigned rot = (unsigned)(s.hi >> 58);                 // state >> 122
     return (x >> rot) | (x << ((64u - rot) & 63u));

@@ -2,13 +2,16 @@
 //
 // One wavefront (64 lanes) owns one board.  The board's int8 colour/type
 // planes live in LDS for the whole call; lanes map to cells for the
-// data-parallel stages (line flags, effective-action scan, refill, colour
-// regeneration, shuffle apply), to columns for gravity, and to 64
-// consecutive PCG64 outputs for random draws.  The order-dependent list logic
-// of the reference (get_colour_lines' perpendicular pass, process_colour_lines,
+// data-parallel stages (line detection by ballot, effective-action scan,
+// gravity scatter, refill, colour regeneration, shuffle apply) and to 64
+// consecutive PCG64 outputs for random draws (jump-ahead).  Detection results
+// stay in wave-uniform ballot masks; the per-env RNG state stays in scalar
+// registers for the whole call.  The order-dependent list logic of the
+// reference (get_colour_lines' perpendicular pass, process_colour_lines,
 // special placement, the recursive activate_special DFS, combination_match)
-// runs on lane 0 against LDS with an explicit stack.  With no specials enabled
-// the whole cascade stays wave-parallel (no lane-0 section).
+// runs on lane 0 against LDS with an explicit stack; it is compiled only into
+// the general kernel variant.  With no specials enabled the lean variant keeps
+// the whole cascade wave-parallel.
 //
 // Reference: akshilpatel/tile-match-gym v1.0.6, src/tile_match_gym/board.py
 // and tile_match_env.py (file:line cited per function).  Bit-exact per seed.
@@ -32,6 +35,14 @@ namespace tmg {
         __builtin_amdgcn_wave_barrier();                         \
     } while (0)
 #endif
+// compiler-only ordering point between a wave's LDS loads and later stores
+#define WFENCE() __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront")
+
+// dynamic LDS of the workgroup (overridable only by the host-side wave
+// emulator in tools/wave_emu, which runs this file under AddressSanitizer)
+#ifndef TMG_SMEM_DECL
+#define TMG_SMEM_DECL(name) extern __shared__ __align__(16) unsigned char name[]
+#endif
 
 enum : int { SP_COOKIE = 1, SP_VLASER = 2, SP_HLASER = 4, SP_BOMB = 8 };
 enum : int { M_NORMAL = 0, M_VLASER = 1, M_HLASER = 2, M_BOMB = 3, M_COOKIE = 4 };
@@ -43,29 +54,33 @@ struct Params {
     const uint64_t *jump;         // [64][4] jump-ahead table
 };
 
-// scalar slots in LDS
+// scalar slots in LDS (lane-0 sections publish through these)
 enum : int { SC_NACT = 0, SC_NNEW, SC_ERR, SC_NZ, SC_A, SC_B, SC_C, SC_D, SC_COUNT = 16 };
 
+template <int MAXN_>
+struct WsCore {
+    static constexpr int MAXN = MAXN_;
+    static constexpr int NP = MAXN / 64;            // 64-cell passes
+    static constexpr int MAXW = (2 * MAXN) / 64 + 2;
+    uint64_t effw[MAXW];
+    int32_t sc[SC_COUNT];
+    int8_t brd[2 * MAXN];          // [colour plane N][type plane N], runtime N (same layout as HBM)
+    uint8_t mark[MAXN];
+    union {
+        uint32_t draw[MAXN + 128];                  // refill colours
+        struct { int8_t tmp[2 * MAXN]; int16_t perm[MAXN]; } sh;   // shuffle
+    } u;
+};
+
 template <int MAXN>
-struct Ws {
+struct WsSerial {                                   // lane-0 list machinery (general variant only)
     static constexpr int POOL = 4 * MAXN + 256;     // coords of lines
     static constexpr int MLINES = MAXN + 64;        // lines
     static constexpr int MQ = 2 * MAXN + 64;        // process queue
     static constexpr int MM = MAXN + 32;            // matches
     static constexpr int MPOOL = 4 * MAXN + 256;    // coords of matches
-    static constexpr int MAXW = (2 * MAXN) / 64 + 2;
-    static constexpr int MSTK = MAXN + 8;
-
-    uint64_t rng[5];
-    uint64_t effw[MAXW];
-    int32_t sc[SC_COUNT];
-    uint32_t draw[MAXN + 128];
-    int8_t brd[2 * MAXN];          // [colour plane N][type plane N], runtime N
-    int8_t tmp[2 * MAXN];
-    uint8_t mark[MAXN];
-    uint8_t flag[MAXN];
-    int16_t perm[MAXN];
-    // lane-0 list machinery (general path)
+    static constexpr int MSTK = MAXN + 8;           // activation DFS frames
+    static constexpr int MV = 96;                   // coords of one match
     int16_t pool[POOL];
     int16_t ls[MLINES], ll[MLINES];
     int16_t q[MQ];
@@ -74,126 +89,161 @@ struct Ws {
     int8_t mname[MM], mcol[MM];
     int16_t fcell[MSTK], fidx[MSTK];
     int8_t ftype[MSTK], faux[MSTK];
+    int16_t valid[MV];
+    int16_t taken[MM], qpos[MM];
+    int8_t qname[MM], qcol[MM];
+    int32_t counts[16];
+    int16_t pick[4];
 };
 
-__device__ inline uint64_t lanemask_lt(int lane) { return lane ? (~0ULL >> (64 - lane)) : 0ULL; }
+template <int MAXN, bool GEN>
+struct Ws : WsCore<MAXN> {};
+template <int MAXN>
+struct Ws<MAXN, true> : WsCore<MAXN> {
+    WsSerial<MAXN> s;
+};
 
-__device__ inline uint64_t rdlane64(uint64_t v, int l) {
+__device__ __forceinline__ uint64_t lanemask_lt(int lane) { return lane ? (~0ULL >> (64 - lane)) : 0ULL; }
+
+__device__ __forceinline__ uint64_t rdlane64(uint64_t v, int l) {
     uint32_t lo = __builtin_amdgcn_readlane((uint32_t)v, l);
     uint32_t hi = __builtin_amdgcn_readlane((uint32_t)(v >> 32), l);
     return ((uint64_t)hi << 32) | lo;
 }
+__device__ __forceinline__ uint64_t bcast64(uint64_t v) {
+    uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v);
+    uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
+    return ((uint64_t)hi << 32) | lo;
+}
+
+// ------------------------------------------------------------------- RNG
+// numpy PCG64 state of one env, wave-uniform: s (128), inc (128),
+// h = has_uint32 << 32 | uinteger.
+struct Rng {
+    uint64_t slo, shi, ilo, ihi, h;
+};
+__device__ __forceinline__ void rng_bcast(Rng &g) {
+    g.slo = bcast64(g.slo); g.shi = bcast64(g.shi); g.ilo = bcast64(g.ilo); g.ihi = bcast64(g.ihi); g.h = bcast64(g.h);
+}
 
 struct LaneJump {
-    U128 Aj, Gj;    // A^{lane+1}, G_{lane+1}
+    U128 Aj, Gj, incG;    // A^{lane+1}, G_{lane+1}, G_{lane+1} * inc
 };
 
-// --------------------------------------------------------------- RNG (LDS state)
-template <int MAXN>
-__device__ inline uint64_t s_next64(Ws<MAXN> &w) {                 // lane-0 serial
-    U128 s{w.rng[0], w.rng[1]}, inc{w.rng[2], w.rng[3]};
-    s = add128(mul128(s, U128{PCG_A_LO, PCG_A_HI}), inc);
-    w.rng[0] = s.lo;
-    w.rng[1] = s.hi;
+// single-lane stream (serial replays, shuffle)
+__device__ __forceinline__ uint64_t r_next64(Rng &g) {
+    U128 s = add128(mul128(U128{g.slo, g.shi}, U128{PCG_A_LO, PCG_A_HI}), U128{g.ilo, g.ihi});
+    g.slo = s.lo; g.shi = s.hi;
     return xsl_rr(s);
 }
-template <int MAXN>
-__device__ inline uint32_t s_next32(Ws<MAXN> &w) {
-    uint64_t h = w.rng[4];
-    if (h >> 32) { w.rng[4] = (uint32_t)h; return (uint32_t)h; }
-    uint64_t n = s_next64(w);
-    w.rng[4] = (1ULL << 32) | (n >> 32);
+__device__ __forceinline__ uint32_t r_next32(Rng &g) {                      // half-word buffer (numpy next_uint32)
+    if (g.h >> 32) { g.h = (uint32_t)g.h; return (uint32_t)g.h; }
+    uint64_t n = r_next64(g);
+    g.h = (1ULL << 32) | (n >> 32);
     return (uint32_t)n;
 }
-template <int MAXN>
-__device__ inline int s_colour(const Params &P, Ws<MAXN> &w) {     // integers(1,k+1) one draw
+__device__ __forceinline__ int r_colour(const Params &P, Rng &g) {         // integers(1, k+1), one value
     uint32_t excl = (uint32_t)P.k;
-    uint64_t m = (uint64_t)s_next32(w) * excl;
+    uint64_t m = (uint64_t)r_next32(g) * excl;
     uint32_t left = (uint32_t)m;
     if (left < excl) {
-        while (left < P.thr) { m = (uint64_t)s_next32(w) * excl; left = (uint32_t)m; }
+        while (left < P.thr) { m = (uint64_t)r_next32(g) * excl; left = (uint32_t)m; }
     }
     return 1 + (int)(m >> 32);
 }
-template <int MAXN>
-__device__ inline uint32_t s_interval(Ws<MAXN> &w, uint32_t max) { // random_interval
+__device__ __forceinline__ uint32_t r_interval(Rng &g, uint32_t max) {     // random_interval
     if (max == 0) return 0;
     uint32_t mask = max;
     mask |= mask >> 1; mask |= mask >> 2; mask |= mask >> 4; mask |= mask >> 8; mask |= mask >> 16;
     uint32_t v;
-    while ((v = (s_next32(w) & mask)) > max) {}
+    while ((v = (r_next32(g) & mask)) > max) {}
     return v;
 }
 
-// w.draw[0..M) <- M colours exactly as Generator.integers(1, k+1, M) (board.py:97,129,239)
-template <int MAXN>
-__device__ void draw_colours(const Params &P, Ws<MAXN> &w, int lane, const LaneJump &J, int M) {
+// dst[0..M) <- Generator.integers(1, k+1, M) (board.py:97,129,239), lane-parallel:
+// lane j evaluates PCG output j of the batch by jump-ahead; the caller syncs.
+template <class T>
+__device__ __forceinline__ void draw_colours(const Params &P, int lane, const LaneJump &J, Rng &g, int M, T *dst) {
     if (M <= 0) return;
-    if (P.k == 1) {                                        // rng == 0: numpy draws nothing
-        for (int i = lane; i < M; i += 64) w.draw[i] = 1;
-        WSYNC();
+    const uint32_t k = (uint32_t)P.k;
+    if (k == 1) {                                          // rng == 0: numpy draws nothing
+        for (int i = lane; i < M; i += 64) dst[i] = (T)1;
         return;
     }
-    const uint64_t s0lo = w.rng[0], s0hi = w.rng[1], ilo = w.rng[2], ihi = w.rng[3], h0 = w.rng[4];
-    const int has = (int)(h0 >> 32) & 1;
-    int off = 0;
-    if (has) { if (lane == 0) w.draw[0] = (uint32_t)h0; off = 1; }
+    const Rng g0 = g;
+    const int off = (int)(g.h >> 32) & 1;
+    bool rej = false;
+    if (off && lane == 0) {
+        uint64_t m = (uint64_t)(uint32_t)g.h * k;
+        dst[0] = (T)(1 + (m >> 32));
+        rej |= (uint32_t)m < P.thr;
+    }
     const int need = M - off;
     const int n64 = (need + 1) >> 1;
-    U128 s{s0lo, s0hi};
-    const U128 incG = mul128(U128{ilo, ihi}, J.Gj);
-    uint64_t last_hi = (uint32_t)h0;
+    U128 s{g.slo, g.shi};
+    uint64_t last_hi = 0;
     for (int base = 0; base < n64; base += 64) {
-        U128 sj = add128(mul128(J.Aj, s), incG);
+        U128 sj = add128(mul128(J.Aj, s), J.incG);
         uint64_t out = xsl_rr(sj);
         int j = base + lane;
         if (j < n64) {
-            int i0 = off + 2 * j;
-            w.draw[i0] = (uint32_t)out;
-            if (2 * j + 1 < need) w.draw[i0 + 1] = (uint32_t)(out >> 32);
+            uint64_t m0 = (uint64_t)(uint32_t)out * k;
+            dst[off + 2 * j] = (T)(1 + (m0 >> 32));
+            rej |= (uint32_t)m0 < P.thr;
+            if (2 * j + 1 < need) {
+                uint64_t m1 = (out >> 32) * k;
+                dst[off + 2 * j + 1] = (T)(1 + (m1 >> 32));
+                rej |= (uint32_t)m1 < P.thr;
+            }
         }
         int cnt = n64 - base < 64 ? n64 - base : 64;
         s.lo = rdlane64(sj.lo, cnt - 1);
         s.hi = rdlane64(sj.hi, cnt - 1);
         last_hi = rdlane64(out >> 32, cnt - 1);
     }
-    WSYNC();
-    // Lemire rejection (numpy buffered_bounded_lemire_uint32): vanishingly rare
-    bool rej = false;
-    if (P.thr) {
-        for (int i = lane; i < M; i += 64) {
-            uint32_t left = (uint32_t)((uint64_t)w.draw[i] * (uint32_t)P.k);
-            rej |= left < P.thr;
+    if (__ballot(rej) != 0ULL) {                           // Lemire rejection: exact serial replay
+        WFENCE();
+        if (lane == 0) {
+            Rng r = g0;
+            for (int i = 0; i < M; i++) dst[i] = (T)r_colour(P, r);
+            g = r;
         }
-    }
-    if (__ballot(rej) != 0ULL) {
-        if (lane == 0) {                                   // exact serial replay
-            w.rng[0] = s0lo; w.rng[1] = s0hi; w.rng[4] = h0;
-            for (int i = 0; i < M; i++) w.draw[i] = (uint32_t)s_colour(P, w);
-        }
-        WSYNC();
+        rng_bcast(g);
         return;
     }
-    for (int i = lane; i < M; i += 64) w.draw[i] = 1u + (uint32_t)(((uint64_t)w.draw[i] * (uint32_t)P.k) >> 32);
-    if (lane == 0) {
-        if (n64 > 0) {
-            w.rng[0] = s.lo; w.rng[1] = s.hi;
-            w.rng[4] = ((uint64_t)(need & 1) << 32) | (uint32_t)last_hi;
-        } else {
-            w.rng[4] = (uint32_t)h0;                       // only the buffered half was used
-        }
+    if (n64 > 0) {
+        g.slo = s.lo; g.shi = s.hi;
+        g.h = ((uint64_t)(need & 1) << 32) | (uint32_t)last_hi;
+    } else {
+        g.h = (uint32_t)g0.h;                              // only the buffered half was used
     }
-    WSYNC();
 }
 
 // --------------------------------------------------------------- board helpers
-__device__ inline void action_coords(int R, int C, int a, int &r1, int &c1, int &r2, int &c2) {  // board.py:77-93
+__device__ __forceinline__ void action_coords(int R, int C, int a, int &r1, int &c1, int &r2, int &c2) {  // board.py:77-93
     if (a < C * (R - 1)) { r1 = a / C; c1 = a % C; r2 = r1 + 1; c2 = c1; }
     else { int i = a - C * (R - 1); r1 = i / (C - 1); c1 = i % (C - 1); r2 = r1; c2 = c1 + 1; }
 }
 
-template <int MAXN>
-__device__ inline void load_board(const Params &P, Ws<MAXN> &w, int lane, const int8_t *src) {
+// per-lane cell coordinates of each 64-cell pass, computed once per kernel
+template <int NP>
+struct Cells {
+    int r[NP], c[NP];
+};
+template <int NP>
+__device__ __forceinline__ Cells<NP> make_cells(const Params &P, int lane) {
+    Cells<NP> cl;
+#pragma unroll
+    for (int i = 0; i < NP; i++) {
+        int p = i * 64 + lane;
+        cl.r[i] = p / P.C;
+        cl.c[i] = p - cl.r[i] * P.C;
+    }
+    return cl;
+}
+
+template <class WS>
+__device__ __forceinline__ void load_board(const Params &P, WS &w, int lane, const int8_t *src) {
     const int nb = 2 * P.N;
     if ((nb & 3) == 0) {
         const uint32_t *s = reinterpret_cast<const uint32_t *>(src);
@@ -203,8 +253,8 @@ __device__ inline void load_board(const Params &P, Ws<MAXN> &w, int lane, const 
         for (int i = lane; i < nb; i += 64) w.brd[i] = src[i];
     }
 }
-template <int MAXN>
-__device__ inline void store_board(const Params &P, const Ws<MAXN> &w, int lane, int8_t *dst) {
+template <class WS>
+__device__ __forceinline__ void store_board(const Params &P, const WS &w, int lane, int8_t *dst) {
     const int nb = 2 * P.N;
     if ((nb & 3) == 0) {
         uint32_t *d = reinterpret_cast<uint32_t *>(dst);
@@ -216,12 +266,11 @@ __device__ inline void store_board(const Params &P, const Ws<MAXN> &w, int lane,
 }
 
 // is_move_effective, board.py:735-787 — exact windowed scan (any board)
-template <int MAXN>
-__device__ bool eff_exact(const Params &P, const Ws<MAXN> &w, int a) {
+__device__ __forceinline__ bool eff_exact(const Params &P, const int8_t *brd, int a) {
     const int R = P.R, C = P.C, N = P.N;
     int r1, c1, r2, c2;
     action_coords(R, C, a, r1, c1, r2, c2);
-    const int8_t *col = w.brd, *typ = w.brd + N;
+    const int8_t *col = brd, *typ = brd + N;
     const int p = r1 * C + c1, q = r2 * C + c2;
     const int tp = typ[p], tq = typ[q];
     if ((tp != 0 && tp != 1) && (tq != 0 && tq != 1)) return true;
@@ -253,12 +302,11 @@ __device__ bool eff_exact(const Params &P, const Ws<MAXN> &w, int a) {
 // Same predicate when the board holds no cookie and no pre-existing colour
 // triple (checked by the caller): only triples through exactly one of the two
 // swapped cells can appear, all inside the reference's window.
-template <int MAXN>
-__device__ bool eff_fast(const Params &P, const Ws<MAXN> &w, int a) {
+__device__ __forceinline__ bool eff_fast(const Params &P, const int8_t *brd, int a) {
     const int R = P.R, C = P.C, N = P.N;
     int r1, c1, r2, c2;
     action_coords(R, C, a, r1, c1, r2, c2);
-    const int8_t *col = w.brd, *typ = w.brd + N;
+    const int8_t *col = brd, *typ = brd + N;
     const int p = r1 * C + c1, q = r2 * C + c2;
     const int tp = typ[p], tq = typ[q];
     if ((tp != 0 && tp != 1) && (tq != 0 && tq != 1)) return true;
@@ -283,144 +331,191 @@ __device__ bool eff_fast(const Params &P, const Ws<MAXN> &w, int a) {
 }
 
 // _get_effective_actions / possible_move (tile_match_env.py:118-124, board.py:558-569):
-// fills w.effw, returns whether any action is effective.
-template <int MAXN>
-__device__ bool scan_effective(const Params &P, Ws<MAXN> &w, int lane) {
+// fills w.effw, returns whether any action is effective.  `clean` = the caller
+// knows the board has no cookie and no colour triple (it just came out of a
+// line-free detection with no cookie enabled), which skips the precheck.
+template <class WS>
+__device__ __forceinline__ bool scan_effective(const Params &P, WS &w, int lane, const Cells<WS::NP> &cl, bool clean) {
     const int R = P.R, C = P.C, N = P.N;
     const int8_t *col = w.brd, *typ = w.brd + N;
-    bool odd = false;          // cookie on board or a pre-existing triple -> exact scan
-    for (int p = lane; p < N; p += 64) {
-        int r = p / C, c = p - r * C, x = col[p];
-        odd |= typ[p] < 0;
-        odd |= (c + 2 < C) && col[p + 1] == x && col[p + 2] == x && typ[p + 2] >= 0;
-        odd |= (r + 2 < R) && col[p + C] == x && col[p + 2 * C] == x && typ[p + 2 * C] >= 0;
+    bool exact = false;
+    if (!clean) {
+        bool odd = false;      // cookie on board or a pre-existing triple -> exact scan
+#pragma unroll
+        for (int i = 0; i < WS::NP; i++) {
+            int p = i * 64 + lane;
+            if (p < N) {
+                int r = cl.r[i], c = cl.c[i], x = col[p];
+                odd |= typ[p] < 0;
+                odd |= (c + 2 < C) && col[p + 1] == x && col[p + 2] == x && typ[p + 2] >= 0;
+                odd |= (r + 2 < R) && col[p + C] == x && col[p + 2 * C] == x && typ[p + 2 * C] >= 0;
+            }
+        }
+        exact = __ballot(odd) != 0ULL;
     }
-    const bool exact = __ballot(odd) != 0ULL;
     uint64_t any = 0;
     for (int base = 0, wi = 0; base < P.A; base += 64, wi++) {
         int a = base + lane;
         bool e = false;
-        if (a < P.A) e = exact ? eff_exact(P, w, a) : eff_fast(P, w, a);
+        if (a < P.A) e = exact ? eff_exact(P, w.brd, a) : eff_fast(P, w.brd, a);
         uint64_t m = __ballot(e);
         if (lane == 0) w.effw[wi] = m;
         any |= m;
     }
-    WSYNC();
     return any != 0ULL;
 }
 
-// Line flags (get_colour_lines' first pass, board.py:158-193):
-// flag bit0 = vertical line anchored here, bit1 = horizontal line may start here.
-// Returns the bottom-most row holding a line, or -1.
-template <int MAXN>
-__device__ int detect_row(const Params &P, Ws<MAXN> &w, int lane) {
-    const int R = P.R, C = P.C, N = P.N;
+// Line masks (get_colour_lines' first pass, board.py:158-193): bit p of v/h =
+// a vertical line is anchored at cell p / a horizontal line may start at p.
+template <int NP>
+struct Det {
+    uint64_t v[NP], h[NP];
+};
+
+template <int NP>
+__device__ __forceinline__ uint64_t bits_at(const uint64_t (&m)[NP], int start, int len) {   // len <= 64
+    const int wi = start >> 6, off = start & 63;
+    uint64_t lo = 0, hi = 0;
+#pragma unroll
+    for (int i = 0; i < NP; i++) {
+        if (i == wi) lo = m[i];
+        if (i == wi + 1) hi = m[i];
+    }
+    uint64_t r = lo >> off;
+    if (off && off + len > 64) r |= hi << (64 - off);
+    return len >= 64 ? r : (r & ((1ULL << len) - 1));
+}
+
+// Returns the bottom-most row holding a line, or -1 (get_colour_lines == []).
+template <class WS>
+__device__ __forceinline__ int detect(const Params &P, const WS &w, int lane, const Cells<WS::NP> &cl, Det<WS::NP> &d) {
+    const int C = P.C, N = P.N;
     const int8_t *col = w.brd, *typ = w.brd + N;
     int pmax = -1;
-    for (int p0 = 0; p0 < N; p0 += 64) {
-        int p = p0 + lane;
-        uint8_t f = 0;
+#pragma unroll
+    for (int i = 0; i < WS::NP; i++) {
+        int p = i * 64 + lane;
+        bool fv = false, fh = false;
         if (p < N) {
-            int r = p / C, c = p - r * C, x = col[p];
+            int r = cl.r[i], c = cl.c[i], x = col[p];
             bool t = typ[p] > 0;
-            if (t && r >= 2 && col[p - C] == x && col[p - 2 * C] == x) f |= 1;
-            if (t && c + 2 < C && col[p + 1] == x && col[p + 2] == x) f |= 2;
-            w.flag[p] = f;
+            fv = t && r >= 2 && col[p - C] == x && col[p - 2 * C] == x;
+            fh = t && c + 2 < C && col[p + 1] == x && col[p + 2] == x;
         }
-        uint64_t m = __ballot(f != 0);
-        if (m) pmax = p0 + 63 - __clzll(m);
+        d.v[i] = __ballot(fv);
+        d.h[i] = __ballot(fh);
+        uint64_t m = d.v[i] | d.h[i];
+        if (m) pmax = i * 64 + 63 - __clzll(m);
     }
-    WSYNC();
-    (void)R;
     return pmax < 0 ? -1 : pmax / C;
 }
 
-// For remove_colour_lines (board.py:120-131): row of the first coord of the
-// first line get_colour_lines would return, or -1 when it returns [].
-template <int MAXN>
-__device__ int first_line_row(const Params &P, Ws<MAXN> &w, int lane) {
+// top row of the same-colour run ending at (rs, c) (vertical line start)
+template <class WS>
+__device__ __forceinline__ int run_top(const Params &P, const WS &w, int lane, int rs, int c) {
     const int C = P.C;
-    const int rs = detect_row(P, w, lane);
-    if (rs < 0) return -1;
-    uint8_t f = lane < C ? w.flag[rs * C + lane] : 0;
-    uint64_t mrow = __ballot(f != 0);
-    int c0 = __ffsll((unsigned long long)mrow) - 1;
-    int fc0 = __builtin_amdgcn_readfirstlane((int)w.flag[rs * C + c0]);
-    if (!(fc0 & 1)) return rs;                            // horizontal line at (rs, c0..)
-    // vertical: the line starts at the top of the same-colour run above rs
-    const int8_t *col = w.brd;
-    int x = col[rs * C + c0];
-    bool neq = lane < rs && col[lane * C + c0] != x;
+    const int x = w.brd[rs * C + c];
+    bool neq = lane < rs && w.brd[lane * C + c] != x;
     uint64_t mn = __ballot(neq);
     return mn ? (63 - __clzll(mn)) + 1 : 0;
 }
 
-// gravity, board.py:217-229 — one lane per column, stable partition
-template <int MAXN>
-__device__ void gravity(const Params &P, Ws<MAXN> &w, int lane) {
+// For remove_colour_lines (board.py:120-131): row of the first coord of the
+// first line get_colour_lines would return, or -1 when it returns [].
+template <class WS>
+__device__ __forceinline__ int first_line_row(const Params &P, const WS &w, int lane, const Cells<WS::NP> &cl) {
+    const int C = P.C;
+    Det<WS::NP> d;
+    const int rs = detect(P, w, lane, cl, d);
+    if (rs < 0) return -1;
+    const uint64_t vb = bits_at(d.v, rs * C, C), hb = bits_at(d.h, rs * C, C);
+    const int c0 = __ffsll((unsigned long long)(vb | hb)) - 1;
+    if (!((vb >> c0) & 1)) return rs;                     // horizontal line at (rs, c0..)
+    return run_top(P, w, lane, rs, c0);                   // vertical: starts at the top of its run
+}
+
+// gravity, board.py:217-229 — stable partition of each column (empties to
+// the top).  Lanes are laid out column-major (64/R columns per pass) so one
+// ballot holds whole columns: a non-empty cell moves down by the popcount of
+// the empties below it, as one scatter.
+template <class WS>
+__device__ __forceinline__ void gravity(const Params &P, WS &w, int lane) {
     const int R = P.R, C = P.C, N = P.N;
     int8_t *col = w.brd, *typ = w.brd + N;
-    if (lane < C) {
-        int wr = R - 1;
-        for (int r = R - 1; r >= 0; r--) {
-            int p = r * C + lane;
-            int8_t a = col[p], t = typ[p];
-            if (!(a == 0 && t == 0)) {
-                int d = wr * C + lane;
-                col[d] = a; typ[d] = t;
-                wr--;
-            }
+    const int cpp = 64 / R;
+    const int lc = lane / R, r = lane - lc * R;
+    const uint64_t colmask = (R == 64 ? ~0ULL : ((1ULL << R) - 1)) << (lc * R);
+    const uint64_t above = lane == 63 ? 0ULL : ~((2ULL << lane) - 1);    // lanes > lane: lower rows
+    for (int c0 = 0; c0 < C; c0 += cpp) {
+        const int c = c0 + lc;
+        const bool in = lc < cpp && c < C;
+        const int p = r * C + c;
+        int8_t a = 0, t = 0;
+        if (in) { a = col[p]; t = typ[p]; }
+        const bool empty = in && a == 0 && t == 0;
+        const uint64_t E = __ballot(empty);
+        if (!E) continue;
+        const int below = __popcll(E & colmask & above);
+        const int total = __popcll(E & colmask);
+        WFENCE();
+        if (in) {
+            if (!empty && below) { int d = p + below * C; col[d] = a; typ[d] = t; }
+            if (r < total) { col[p] = 0; typ[p] = 0; }
         }
-        for (int r = wr; r >= 0; r--) { col[r * C + lane] = 0; typ[r * C + lane] = 0; }
+        WFENCE();
     }
-    WSYNC();
 }
 
 // refill, board.py:231-241 — empties in row-major order get consecutive draws
-template <int MAXN>
-__device__ void refill(const Params &P, Ws<MAXN> &w, int lane, const LaneJump &J) {
+template <class WS>
+__device__ __forceinline__ void refill(const Params &P, WS &w, int lane, const LaneJump &J, Rng &g) {
     const int N = P.N;
     int8_t *col = w.brd, *typ = w.brd + N;
+    uint64_t E[WS::NP];
     int total = 0;
-    for (int p0 = 0; p0 < N; p0 += 64) {
-        int p = p0 + lane;
-        bool e = p < N && col[p] == 0 && typ[p] == 0;
-        total += __popcll(__ballot(e));
+#pragma unroll
+    for (int i = 0; i < WS::NP; i++) {
+        int p = i * 64 + lane;
+        E[i] = __ballot(p < N && col[p] == 0 && typ[p] == 0);
+        total += __popcll(E[i]);
     }
     if (total == 0) return;
-    draw_colours(P, w, lane, J, total);
+    draw_colours(P, lane, J, g, total, w.u.draw);
+    WSYNC();
     int base = 0;
-    for (int p0 = 0; p0 < N; p0 += 64) {
-        int p = p0 + lane;
-        bool e = p < N && col[p] == 0 && typ[p] == 0;
-        uint64_t m = __ballot(e);
-        if (e) {
-            int idx = base + __popcll(m & lanemask_lt(lane));
-            col[p] = (int8_t)w.draw[idx];
+#pragma unroll
+    for (int i = 0; i < WS::NP; i++) {
+        int p = i * 64 + lane;
+        if ((E[i] >> lane) & 1) {
+            int idx = base + __popcll(E[i] & lanemask_lt(lane));
+            col[p] = (int8_t)w.u.draw[idx];
             typ[p] = 1;
         }
-        base += __popcll(m);
+        base += __popcll(E[i]);
     }
     WSYNC();
 }
 
-// shuffle, board.py:114-118
-template <int MAXN>
-__device__ void shuffle(const Params &P, Ws<MAXN> &w, int lane) {
+// shuffle, board.py:114-118 (both planes)
+template <class WS>
+__device__ __forceinline__ void shuffle(const Params &P, WS &w, int lane, Rng &g) {
     const int N = P.N;
     if (lane == 0) {
-        for (int i = 0; i < N; i++) w.perm[i] = (int16_t)i;
+        Rng r = g;
+        for (int i = 0; i < N; i++) w.u.sh.perm[i] = (int16_t)i;
         for (int i = N - 1; i >= 1; i--) {
-            int j = (int)s_interval(w, (uint32_t)i);
-            int16_t x = w.perm[i]; w.perm[i] = w.perm[j]; w.perm[j] = x;
+            int j = (int)r_interval(r, (uint32_t)i);
+            int16_t x = w.u.sh.perm[i]; w.u.sh.perm[i] = w.u.sh.perm[j]; w.u.sh.perm[j] = x;
         }
+        g = r;
     }
-    for (int i = lane; i < 2 * N; i += 64) w.tmp[i] = w.brd[i];
+    rng_bcast(g);
+    for (int i = lane; i < 2 * N; i += 64) w.u.sh.tmp[i] = w.brd[i];
     WSYNC();
     for (int p = lane; p < N; p += 64) {
-        int s = w.perm[p];
-        w.brd[p] = w.tmp[s];
-        w.brd[N + p] = w.tmp[N + s];
+        int s = w.u.sh.perm[p];
+        w.brd[p] = w.u.sh.tmp[s];
+        w.brd[N + p] = w.u.sh.tmp[N + s];
     }
     WSYNC();
 }
@@ -428,51 +523,54 @@ __device__ void shuffle(const Params &P, Ws<MAXN> &w, int lane) {
 // generate_board's / move's "while not possible_move() or lines" loop
 // (board.py:102-109, 381-391, remove_colour_lines :120-131).  Leaves the final
 // board's effective mask in w.effw.  Returns true when a shuffle ran.
-template <int MAXN>
-__device__ bool ensure_playable(const Params &P, Ws<MAXN> &w, int lane, const LaneJump &J) {
+template <class WS>
+__device__ __forceinline__ bool ensure_playable(const Params &P, WS &w, int lane, const LaneJump &J, Rng &g,
+                                const Cells<WS::NP> &cl) {
     bool shuffled = false;
     for (;;) {
         for (;;) {
-            int r0 = first_line_row(P, w, lane);
+            int r0 = first_line_row(P, w, lane, cl);
             if (r0 < 0) break;
-            int row = P.R - 1 < r0 + 1 ? P.R - 1 : r0 + 1;
-            int M = (row + 1) * P.C;
-            draw_colours(P, w, lane, J, M);
-            for (int p = lane; p < M; p += 64) w.brd[p] = (int8_t)w.draw[p];
+            int row = P.R - 1 < r0 + 1 ? P.R - 1 : r0 + 1;   // colour plane only, rows 0..row
+            draw_colours(P, lane, J, g, (row + 1) * P.C, w.brd);
             WSYNC();
         }
-        if (scan_effective(P, w, lane)) break;
-        shuffle(P, w, lane);
+        if (scan_effective(P, w, lane, cl, (P.smask & SP_COOKIE) == 0)) break;
+        WSYNC();
+        shuffle(P, w, lane, g);
         shuffled = true;
     }
+    WSYNC();
     return shuffled;
 }
 
 // generate_board, board.py:95-109
-template <int MAXN>
-__device__ void generate_board(const Params &P, Ws<MAXN> &w, int lane, const LaneJump &J) {
+template <class WS>
+__device__ __forceinline__ void generate_board(const Params &P, WS &w, int lane, const LaneJump &J, Rng &g, const Cells<WS::NP> &cl) {
     const int N = P.N;
-    draw_colours(P, w, lane, J, N);
-    for (int p = lane; p < N; p += 64) { w.brd[p] = (int8_t)w.draw[p]; w.brd[N + p] = 1; }
+    draw_colours(P, lane, J, g, N, w.brd);
+    for (int p = lane; p < N; p += 64) w.brd[N + p] = 1;
     WSYNC();
-    ensure_playable(P, w, lane, J);
+    ensure_playable(P, w, lane, J, g, cl);
 }
 
-template <int MAXN>
-__device__ int count_type_zero(const Params &P, Ws<MAXN> &w, int lane) {
+template <class WS>
+__device__ __forceinline__ int count_type_zero(const Params &P, const WS &w, int lane) {
     int z = 0;
-    for (int p0 = 0; p0 < P.N; p0 += 64) {
-        int p = p0 + lane;
+#pragma unroll
+    for (int i = 0; i < WS::NP; i++) {
+        int p = i * 64 + lane;
         z += __popcll(__ballot(p < P.N && w.brd[P.N + p] == 0));
     }
     return z;
 }
 
-template <int MAXN>
-__device__ int count_colour_nonzero(const Params &P, Ws<MAXN> &w, int lane) {
+template <class WS>
+__device__ __forceinline__ int count_colour_nonzero(const Params &P, const WS &w, int lane) {
     int z = 0;
-    for (int p0 = 0; p0 < P.N; p0 += 64) {
-        int p = p0 + lane;
+#pragma unroll
+    for (int i = 0; i < WS::NP; i++) {
+        int p = i * 64 + lane;
         z += __popcll(__ballot(p < P.N && w.brd[p] != 0));
     }
     return z;
@@ -480,38 +578,28 @@ __device__ int count_colour_nonzero(const Params &P, Ws<MAXN> &w, int lane) {
 
 // ---------------------------------------------------------------- fast cascade
 // One cascade iteration when no special can exist (no specials enabled and
-// every type is 1): the reference then turns every line of
-// get_colour_lines (first pass + perpendicular pass, board.py:149-215) into a
-// normal match (process_colour_lines :269-327) and clears their union
+// every type is 1): the reference then turns every line of get_colour_lines
+// (first pass + perpendicular pass, board.py:149-215) into a normal match
+// (process_colour_lines :269-327) and clears their union
 // (resolve_colour_match :460-471).  Returns the number of cleared cells.
-template <int MAXN>
-__device__ int fast_clear(const Params &P, Ws<MAXN> &w, int lane, int rs) {
+template <class WS>
+__device__ __forceinline__ int fast_clear(const Params &P, WS &w, int lane, const Cells<WS::NP> &cl, const Det<WS::NP> &d, int rs) {
     const int R = P.R, C = P.C, N = P.N;
     int8_t *col = w.brd, *typ = w.brd + N;
-    // mark bit0: first-pass coord (static coords list), bit1: cleared
+    // mark bit0: first-pass coord (the static `coords` list), bit1: cleared
     for (int p = lane; p < N; p += 64) w.mark[p] = 0;
     WSYNC();
-    // horizontal: cells of row rs inside a same-colour run of length >= 3
-    {
-        bool e = lane + 1 < C && col[rs * C + lane] == col[rs * C + lane + 1];
-        uint64_t em = __ballot(e);
-        uint64_t t = em & (em >> 1);
-        uint64_t cov = t | (t << 1) | (t << 2);
-        if (lane < C && ((cov >> lane) & 1)) w.mark[rs * C + lane] = 3;
-    }
-    // vertical: runs of length >= 3 whose bottom is row rs
-    {
-        uint8_t f = lane < C ? w.flag[rs * C + lane] : 0;
-        uint64_t vm = __ballot(f & 1);
-        while (vm) {
-            int c = __ffsll((unsigned long long)vm) - 1;
-            vm &= vm - 1;
-            int x = col[rs * C + c];
-            bool neq = lane < rs && col[lane * C + c] != x;
-            uint64_t mn = __ballot(neq);
-            int top = mn ? (63 - __clzll(mn)) + 1 : 0;
-            if (lane >= top && lane <= rs) w.mark[lane * C + c] = 3;
-        }
+    // horizontal lines of row rs: runs of >= 3 starting at their h bits
+    const uint64_t hb = bits_at(d.h, rs * C, C);
+    const uint64_t cov = hb | (hb << 1) | (hb << 2);
+    if (lane < C && ((cov >> lane) & 1)) w.mark[rs * C + lane] = 3;
+    // vertical lines anchored in row rs: the whole run above
+    uint64_t vb = bits_at(d.v, rs * C, C);
+    while (vb) {
+        int c = __ffsll((unsigned long long)vb) - 1;
+        vb &= vb - 1;
+        int top = run_top(P, w, lane, rs, c);
+        if (lane >= top && lane <= rs) w.mark[lane * C + c] = 3;
     }
     WSYNC();
     // perpendicular pass: from every first-pass coord walk both axes over
@@ -535,8 +623,9 @@ __device__ int fast_clear(const Params &P, Ws<MAXN> &w, int lane, int rs) {
     }
     WSYNC();
     int cleared = 0;
-    for (int p0 = 0; p0 < N; p0 += 64) {
-        int p = p0 + lane;
+#pragma unroll
+    for (int i = 0; i < WS::NP; i++) {
+        int p = i * 64 + lane;
         bool clr = p < N && (w.mark[p] & 2);
         if (clr) { col[p] = 0; typ[p] = 0; }
         cleared += __popcll(__ballot(clr));
@@ -550,28 +639,28 @@ __device__ int fast_clear(const Params &P, Ws<MAXN> &w, int lane, int rs) {
 template <int MAXN>
 struct Serial {
     const Params &P;
-    Ws<MAXN> &w;
+    WsCore<MAXN> &w;
+    WsSerial<MAXN> &s;
     int8_t *col, *typ;
     int R, C, N;
     int nl, np;        // lines / pool fill
     int nm, nmp;       // matches / match-pool fill
     bool ovf;
 
-    __device__ Serial(const Params &P_, Ws<MAXN> &w_) : P(P_), w(w_) {
+    __device__ __forceinline__ Serial(const Params &P_, WsCore<MAXN> &w_, WsSerial<MAXN> &s_) : P(P_), w(w_), s(s_) {
         R = P.R; C = P.C; N = P.N;
         col = w.brd; typ = w.brd + N;
         nl = np = nm = nmp = 0;
         ovf = false;
     }
 
-    __device__ void clr(int p) {
+    __device__ __forceinline__ void clr(int p) {
         if (col[p] != 0) w.sc[SC_NZ]--;
         col[p] = 0; typ[p] = 0;
     }
 
     // ---- get_colour_lines, board.py:149-215 (rs = bottom-most row with a line)
-    __device__ bool push_line_begin() { return nl < Ws<MAXN>::MLINES; }
-    __device__ void build_lines(int rs) {
+    __device__ __forceinline__ void build_lines(int rs) {
         nl = 0; np = 0;
         uint64_t hcov = 0;
         const int row = rs;
@@ -581,9 +670,9 @@ struct Serial {
                 int start = row - 1;
                 while (start > 0 && col[(start - 1) * C + c] == col[p]) start--;
                 if (row - start >= 2) {
-                    if (nl >= Ws<MAXN>::MLINES || np + (row - start + 1) > Ws<MAXN>::POOL) { ovf = true; return; }
-                    w.ls[nl] = (int16_t)np; w.ll[nl] = (int16_t)(row - start + 1);
-                    for (int i = start; i <= row; i++) w.pool[np++] = (int16_t)(i * C + c);
+                    if (nl >= WsSerial<MAXN>::MLINES || np + (row - start + 1) > WsSerial<MAXN>::POOL) { ovf = true; return; }
+                    s.ls[nl] = (int16_t)np; s.ll[nl] = (int16_t)(row - start + 1);
+                    for (int i = start; i <= row; i++) s.pool[np++] = (int16_t)(i * C + c);
                     nl++;
                 }
             }
@@ -591,152 +680,152 @@ struct Serial {
                 int end = c + 1;
                 while (end < C - 1 && col[row * C + end + 1] == col[p]) end++;
                 if (end - c >= 2) {
-                    if (nl >= Ws<MAXN>::MLINES || np + (end - c + 1) > Ws<MAXN>::POOL) { ovf = true; return; }
-                    w.ls[nl] = (int16_t)np; w.ll[nl] = (int16_t)(end - c + 1);
-                    for (int i = c; i <= end; i++) { w.pool[np++] = (int16_t)(row * C + i); hcov |= 1ULL << i; }
+                    if (nl >= WsSerial<MAXN>::MLINES || np + (end - c + 1) > WsSerial<MAXN>::POOL) { ovf = true; return; }
+                    s.ls[nl] = (int16_t)np; s.ll[nl] = (int16_t)(end - c + 1);
+                    for (int i = c; i <= end; i++) { s.pool[np++] = (int16_t)(row * C + i); hcov |= 1ULL << i; }
                     nl++;
                 }
             }
         }
         // perpendicular pass over the static coord list, :195-214
         const int ncoords = np;
-        for (int i = 0; i < ncoords; i++) w.mark[w.pool[i]] = 1;
+        for (int i = 0; i < ncoords; i++) w.mark[s.pool[i]] = 1;
         // directions (0,1),(1,0),(0,-1),(-1,0): the last two walk the same cells
         // as the first two, so their sorted lines are always duplicates
         for (int ci = 0; ci < ncoords && !ovf; ci++) {
-            const int cp = w.pool[ci];
+            const int cp = s.pool[ci];
             const int cr = cp / C, cc = cp - cr * C;
             for (int d = 0; d < 2; d++) {
                 const int st = np;
-                if (np + R + C + 1 > Ws<MAXN>::POOL || nl >= Ws<MAXN>::MLINES) { ovf = true; break; }
-                w.pool[np++] = (int16_t)cp;
-                for (int s = 0; s < 2; s++) {
-                    int dr = d == 1 ? (s ? -1 : 1) : 0, dc = d == 0 ? (s ? -1 : 1) : 0;
+                if (np + R + C + 1 > WsSerial<MAXN>::POOL || nl >= WsSerial<MAXN>::MLINES) { ovf = true; break; }
+                s.pool[np++] = (int16_t)cp;
+                for (int sd = 0; sd < 2; sd++) {
+                    int dr = d == 1 ? (sd ? -1 : 1) : 0, dc = d == 0 ? (sd ? -1 : 1) : 0;
                     int nr = cr + dr, nc = cc + dc;
                     while (nr >= 0 && nr < R && nc >= 0 && nc < C) {
                         int cell = nr * C + nc;
                         if (w.mark[cell]) break;                                    // n in coords
                         if (!(col[cp] == col[cell] && typ[cp] > 0 && typ[cell] > 0)) break;   // match_color
-                        w.pool[np++] = (int16_t)cell;
+                        s.pool[np++] = (int16_t)cell;
                         nr += dr; nc += dc;
                     }
                 }
                 const int len = np - st;
                 if (len >= 3) {
                     for (int i = st + 1; i < np; i++) {                             // sorted()
-                        int16_t x = w.pool[i]; int j = i - 1;
-                        while (j >= st && w.pool[j] > x) { w.pool[j + 1] = w.pool[j]; j--; }
-                        w.pool[j + 1] = x;
+                        int16_t x = s.pool[i]; int j = i - 1;
+                        while (j >= st && s.pool[j] > x) { s.pool[j + 1] = s.pool[j]; j--; }
+                        s.pool[j + 1] = x;
                     }
                     bool dup = false;                                               // not in lines
                     for (int l = 0; l < nl && !dup; l++) {
-                        if (w.ll[l] != len) continue;
+                        if (s.ll[l] != len) continue;
                         bool same = true;
-                        for (int i = 0; i < len; i++) if (w.pool[w.ls[l] + i] != w.pool[st + i]) { same = false; break; }
+                        for (int i = 0; i < len; i++) if (s.pool[s.ls[l] + i] != s.pool[st + i]) { same = false; break; }
                         dup = same;
                     }
                     if (dup) np = st;
-                    else { w.ls[nl] = (int16_t)st; w.ll[nl] = (int16_t)len; nl++; }
+                    else { s.ls[nl] = (int16_t)st; s.ll[nl] = (int16_t)len; nl++; }
                 } else {
                     np = st;
                 }
             }
         }
-        for (int i = 0; i < ncoords; i++) w.mark[w.pool[i]] = 0;
+        for (int i = 0; i < ncoords; i++) w.mark[s.pool[i]] = 0;
     }
 
-    __device__ bool line_has(int l, int cell) {
-        for (int i = 0; i < w.ll[l]; i++) if (w.pool[w.ls[l] + i] == cell) return true;
+    __device__ __forceinline__ bool line_has(int l, int cell) {
+        for (int i = 0; i < s.ll[l]; i++) if (s.pool[s.ls[l] + i] == cell) return true;
         return false;
     }
 
-    __device__ int add_match(int name, int colour) {
-        if (nm >= Ws<MAXN>::MM) { ovf = true; return -1; }
-        w.ms[nm] = (int16_t)nmp; w.mlen[nm] = 0; w.mname[nm] = (int8_t)name; w.mcol[nm] = (int8_t)colour;
+    __device__ __forceinline__ int add_match(int name, int colour) {
+        if (nm >= WsSerial<MAXN>::MM) { ovf = true; return -1; }
+        s.ms[nm] = (int16_t)nmp; s.mlen[nm] = 0; s.mname[nm] = (int8_t)name; s.mcol[nm] = (int8_t)colour;
         return nm++;
     }
-    __device__ void match_push(int m, int cell) {
-        if (nmp >= Ws<MAXN>::MPOOL) { ovf = true; return; }
-        w.mpool[nmp++] = (int16_t)cell; w.mlen[m]++;
+    __device__ __forceinline__ void match_push(int m, int cell) {
+        if (nmp >= WsSerial<MAXN>::MPOOL) { ovf = true; return; }
+        s.mpool[nmp++] = (int16_t)cell; s.mlen[m]++;
     }
 
     // ---- process_colour_lines, board.py:269-327
-    __device__ void process_lines() {
+    __device__ __forceinline__ void process_lines() {
         const int S = P.smask;
         nm = 0; nmp = 0;
         // lines are already sorted internally; stable sort by first row (:282)
         int qn = 0;
         for (int l = 0; l < nl; l++) {
-            int key = w.pool[w.ls[l]] / C, j = qn - 1;
-            while (j >= 0 && w.pool[w.ls[w.q[j]]] / C > key) { w.q[j + 1] = w.q[j]; j--; }
-            w.q[j + 1] = (int16_t)l;
+            int key = s.pool[s.ls[l]] / C, j = qn - 1;
+            while (j >= 0 && s.pool[s.ls[s.q[j]]] / C > key) { s.q[j + 1] = s.q[j]; j--; }
+            s.q[j + 1] = (int16_t)l;
             qn++;
         }
         int head = 0;
         while (head < qn && !ovf) {
-            const int L = w.q[head++];                                              // pop(0)
-            const int ls = w.ls[L], ln = w.ll[L];
+            const int L = s.q[head++];                                              // pop(0)
+            const int ls = s.ls[L], ln = s.ll[L];
             if (ln >= 5 && (S & SP_COOKIE)) {                                       // :287-292
                 int m = add_match(M_COOKIE, 0); if (m < 0) return;
-                for (int i = 0; i < 5; i++) match_push(m, w.pool[ls + i]);
+                for (int i = 0; i < 5; i++) match_push(m, s.pool[ls + i]);
                 if (ln - 5 > 2) {
-                    if (nl >= Ws<MAXN>::MLINES || qn >= Ws<MAXN>::MQ) { ovf = true; return; }
-                    w.ls[nl] = (int16_t)(ls + 5); w.ll[nl] = (int16_t)(ln - 5);
-                    w.q[qn++] = (int16_t)nl; nl++;
+                    if (nl >= WsSerial<MAXN>::MLINES || qn >= WsSerial<MAXN>::MQ) { ovf = true; return; }
+                    s.ls[nl] = (int16_t)(ls + 5); s.ll[nl] = (int16_t)(ln - 5);
+                    s.q[qn++] = (int16_t)nl; nl++;
                 }
             } else if (ln == 4) {                                                   // :294-302
                 int name;
-                if (w.pool[ls] / C == w.pool[ls + 1] / C && (S & SP_HLASER)) name = M_HLASER;
+                if (s.pool[ls] / C == s.pool[ls + 1] / C && (S & SP_HLASER)) name = M_HLASER;
                 else if (S & SP_VLASER) name = M_VLASER;
                 else name = M_NORMAL;
-                int m = add_match(name, col[w.pool[ls]]); if (m < 0) return;
-                for (int i = 0; i < 4; i++) match_push(m, w.pool[ls + i]);
+                int m = add_match(name, col[s.pool[ls]]); if (m < 0) return;
+                for (int i = 0; i < 4; i++) match_push(m, s.pool[ls + i]);
             } else {
                 bool shared_any = false;
                 if (S & SP_BOMB)
                     for (int h = head; h < qn && !shared_any; h++)
-                        for (int i = 0; i < ln; i++) if (line_has(w.q[h], w.pool[ls + i])) { shared_any = true; break; }
+                        for (int i = 0; i < ln; i++) if (line_has(s.q[h], s.pool[ls + i])) { shared_any = true; break; }
                 if (shared_any) {                                                   // :304-320
                     for (int h = head; h < qn; h++) {
-                        const int O = w.q[h];
+                        const int O = s.q[h];
                         int shared = -1;
-                        for (int i = 0; i < ln; i++) if (line_has(O, w.pool[ls + i])) { shared = w.pool[ls + i]; break; }
+                        for (int i = 0; i < ln; i++) if (line_has(O, s.pool[ls + i])) { shared = s.pool[ls + i]; break; }
                         if (shared < 0) continue;
                         const int sr = shared / C, scc = shared - sr * C;
-                        const int os = w.ls[O], on = w.ll[O];
+                        const int os = s.ls[O], on = s.ll[O];
                         // three closest coords of O (stable sort by manhattan distance)
-                        int pick[3], npk = 0;
+                        int16_t *pick = s.pick; int npk = 0;
                         {
                             int lastd = -1, lasti = -1;
                             for (int t = 0; t < 3 && t < on; t++) {
                                 int bd = 1 << 30, bi = -1;
                                 for (int i = 0; i < on; i++) {
-                                    int v = w.pool[os + i];
+                                    int v = s.pool[os + i];
                                     int d = abs(v / C - sr) + abs(v % C - scc);
                                     bool after = d > lastd || (d == lastd && i > lasti);
                                     if (after && d < bd) { bd = d; bi = i; }
                                 }
-                                pick[npk++] = w.pool[os + bi];
+                                pick[npk++] = s.pool[os + bi];
                                 lastd = bd; lasti = bi;
                             }
                         }
-                        int m = add_match(M_BOMB, col[w.pool[ls]]); if (m < 0) return;
-                        for (int i = 0; i < ln; i++) match_push(m, w.pool[ls + i]);
+                        int m = add_match(M_BOMB, col[s.pool[ls]]); if (m < 0) return;
+                        for (int i = 0; i < ln; i++) match_push(m, s.pool[ls + i]);
                         for (int t = 0; t < npk; t++) {
                             bool inl = false;
-                            for (int i = 0; i < ln; i++) if (w.pool[ls + i] == pick[t]) { inl = true; break; }
+                            for (int i = 0; i < ln; i++) if (s.pool[ls + i] == pick[t]) { inl = true; break; }
                             if (!inl) match_push(m, pick[t]);
                         }
                         if (on < 6) {                                               // lines.remove(l)
-                            for (int j = h; j < qn - 1; j++) w.q[j] = w.q[j + 1];
+                            for (int j = h; j < qn - 1; j++) s.q[j] = s.q[j + 1];
                             qn--;
                         } else {                                                    // l.remove(c) in place
                             for (int t = 0; t < npk; t++) {
-                                int n = w.ll[O];
+                                int n = s.ll[O];
                                 for (int i = 0; i < n; i++)
-                                    if (w.pool[os + i] == pick[t]) {
-                                        for (int u = i; u < n - 1; u++) w.pool[os + u] = w.pool[os + u + 1];
-                                        w.ll[O] = (int16_t)(n - 1);
+                                    if (s.pool[os + i] == pick[t]) {
+                                        for (int u = i; u < n - 1; u++) s.pool[os + u] = s.pool[os + u + 1];
+                                        s.ll[O] = (int16_t)(n - 1);
                                         break;
                                     }
                             }
@@ -744,8 +833,8 @@ struct Serial {
                         break;
                     }
                 } else if (ln >= 3) {                                               // :322-325
-                    int m = add_match(M_NORMAL, col[w.pool[ls]]); if (m < 0) return;
-                    for (int i = 0; i < ln; i++) match_push(m, w.pool[ls + i]);
+                    int m = add_match(M_NORMAL, col[s.pool[ls]]); if (m < 0) return;
+                    for (int i = 0; i < ln; i++) match_push(m, s.pool[ls + i]);
                 }
             }
         }
@@ -754,16 +843,16 @@ struct Serial {
     // ---- activate_special, board.py:473-556, as an explicit DFS
     // frame kinds: 2 v-laser sweep, 3 h-laser sweep, 4 bomb 3x3, -1 cookie scan
     int sp;
-    __device__ void enter(int cell, int t, bool combo) {
+    __device__ __forceinline__ void enter(int cell, int t, bool combo) {
         if (w.sc[SC_NZ] == 0) return;                        // :488-489 np.all(colour == 0)
         if (t == 0 || t == 1) { w.sc[SC_ERR] = 1; return; }  // :491-492
         clr(cell);                                           // :496
         if (!combo) w.sc[SC_NACT]++;                         // :498-499
-        if (sp >= Ws<MAXN>::MSTK) { ovf = true; return; }
+        if (sp >= WsSerial<MAXN>::MSTK) { ovf = true; return; }
         if (t == 2 || t == 3 || t == 4) {
-            w.fcell[sp] = (int16_t)cell; w.ftype[sp] = (int8_t)t; w.fidx[sp] = 0; w.faux[sp] = 0; sp++;
+            s.fcell[sp] = (int16_t)cell; s.ftype[sp] = (int8_t)t; s.fidx[sp] = 0; s.faux[sp] = 0; sp++;
         } else if (t == -1) {                                // :530-545
-            int counts[16];
+            int32_t *counts = s.counts;
             for (int i = 0; i < 16; i++) counts[i] = 0;
             int any = 0, big = 0;
             for (int p = 0; p < N; p++) {
@@ -775,18 +864,18 @@ struct Serial {
             int mcc = 0;
             for (int v = 1; v < 16; v++) if (counts[v] > counts[mcc]) mcc = v;
             for (int p = 0; p < N; p++) if (col[p] == mcc && typ[p] == 1) clr(p);
-            w.fcell[sp] = (int16_t)cell; w.ftype[sp] = -1; w.fidx[sp] = 0; w.faux[sp] = (int8_t)mcc; sp++;
+            s.fcell[sp] = (int16_t)cell; s.ftype[sp] = -1; s.fidx[sp] = 0; s.faux[sp] = (int8_t)mcc; sp++;
         } else {
             w.sc[SC_ERR] = 3;                                // :555-556
         }
     }
-    __device__ void run_dfs() {
+    __device__ __forceinline__ void run_dfs() {
         while (sp > 0 && !ovf && !w.sc[SC_ERR]) {
             const int f = sp - 1;
-            const int t = w.ftype[f];
-            const int cell = w.fcell[f];
+            const int t = s.ftype[f];
+            const int cell = s.fcell[f];
             const int r = cell / C, c = cell - r * C;
-            int idx = w.fidx[f];
+            int idx = s.fidx[f];
             int target = -1;
             if (t == 2) {                                    // :502-507 column sweep
                 if (idx >= R) { sp--; continue; }
@@ -801,45 +890,45 @@ struct Serial {
                 if (idx >= (r1 - r0 + 1) * wdt) { sp--; continue; }
                 target = (r0 + idx / wdt) * C + c0 + idx % wdt;
             } else {                                         // :546-554 cookie: same-colour specials
-                const int mcc = w.faux[f];
+                const int mcc = s.faux[f];
                 while (idx < N && !(typ[idx] > 1 && col[idx] == mcc)) idx++;
                 if (idx >= N) { sp--; continue; }
-                w.fidx[f] = (int16_t)(idx + 1);
+                s.fidx[f] = (int16_t)(idx + 1);
                 enter(idx, typ[idx], false);
                 continue;
             }
-            w.fidx[f] = (int16_t)(idx + 1);
+            s.fidx[f] = (int16_t)(idx + 1);
             int tt = typ[target];
             if (tt != 0 && tt != 1) enter(target, tt, false);
             else clr(target);
         }
     }
-    __device__ void activate(int cell, int t, bool combo) {
+    __device__ __forceinline__ void activate(int cell, int t, bool combo) {
         sp = 0;
         enter(cell, t, combo);
         run_dfs();
     }
 
     // ---- get_special_creation_pos, board.py:429-458
-    __device__ int creation_pos(int m, const int16_t *taken, int nt, bool straight) {
-        const int ms = w.ms[m], ml = w.mlen[m];
-        int valid[64]; int nv = 0;
+    __device__ __forceinline__ int creation_pos(int m, const int16_t *taken, int nt, bool straight) {
+        const int ms = s.ms[m], ml = s.mlen[m];
+        int16_t *valid = s.valid; int nv = 0;
         for (int i = 0; i < ml; i++) {
-            int v = w.mpool[ms + i]; bool tk = false;
+            int v = s.mpool[ms + i]; bool tk = false;
             for (int j = 0; j < nt; j++) if (taken[j] == v) { tk = true; break; }
-            if (!tk && nv < 64) valid[nv++] = v;
+            if (!tk && nv < WsSerial<MAXN>::MV) valid[nv++] = (int16_t)v;
         }
         if (!straight) {
             int br = -1, bc = -1, bnr = -1, bnc = -1;
             for (int i = 0; i < ml; i++) {
-                int v = w.mpool[ms + i], r = v / C, c = v % C, nr = 0, nc = 0;
-                for (int j = 0; j < ml; j++) { int u = w.mpool[ms + j]; nr += (u / C == r); nc += (u % C == c); }
+                int v = s.mpool[ms + i], r = v / C, c = v % C, nr = 0, nc = 0;
+                for (int j = 0; j < ml; j++) { int u = s.mpool[ms + j]; nr += (u / C == r); nc += (u % C == c); }
                 if (nr > bnr) { bnr = nr; br = r; }
                 if (nc > bnc) { bnc = nc; bc = c; }
             }
             int corner = br * C + bc;
             for (int i = 0; i < nv; i++) if (valid[i] == corner) return corner;
-            if (nv == 0) { w.sc[SC_ERR] = 4; return w.mpool[ms]; }
+            if (nv == 0) { w.sc[SC_ERR] = 4; return s.mpool[ms]; }
             int best = 0, bd = 1 << 30;
             for (int i = 0; i < nv; i++) {
                 int dr = valid[i] / C - br, dc = valid[i] % C - bc, d = dr * dr + dc * dc;
@@ -847,9 +936,9 @@ struct Serial {
             }
             return valid[best];
         }
-        if (nv == 0) { w.sc[SC_ERR] = 4; return w.mpool[ms]; }
+        if (nv == 0) { w.sc[SC_ERR] = 4; return s.mpool[ms]; }
         for (int i = 1; i < nv; i++) {
-            int x = valid[i], j = i - 1;
+            int16_t x = valid[i]; int j = i - 1;
             while (j >= 0 && valid[j] > x) { valid[j + 1] = valid[j]; j--; }
             valid[j + 1] = x;
         }
@@ -857,39 +946,39 @@ struct Serial {
     }
 
     // ---- resolve_colour_matches, board.py:397-427 (+ resolve_colour_match :460-471, create_special :572-597)
-    __device__ void resolve() {
-        int16_t taken[64]; int nt = 0;
-        int qpos[64], qname[64], qcol[64], nq = 0;
+    __device__ __forceinline__ void resolve() {
+        int16_t *taken = s.taken; int nt = 0;
+        int16_t *qpos = s.qpos; int8_t *qname = s.qname, *qcol = s.qcol; int nq = 0;
         for (int m = 0; m < nm; m++) {
-            if (w.mname[m] == M_NORMAL) continue;
-            if (nq >= 64) { ovf = true; return; }
-            int pos = creation_pos(m, taken, nt, w.mname[m] != M_BOMB);
+            if (s.mname[m] == M_NORMAL) continue;
+            if (nq >= WsSerial<MAXN>::MM) { ovf = true; return; }
+            int pos = creation_pos(m, taken, nt, s.mname[m] != M_BOMB);
             bool dup = false;
             for (int j = 0; j < nt; j++) if (taken[j] == pos) dup = true;
-            if (!dup && nt < 64) taken[nt++] = (int16_t)pos;
-            qpos[nq] = pos; qname[nq] = w.mname[m]; qcol[nq] = w.mcol[m]; nq++;
+            if (!dup) taken[nt++] = (int16_t)pos;
+            qpos[nq] = (int16_t)pos; qname[nq] = s.mname[m]; qcol[nq] = s.mcol[m]; nq++;
         }
         for (int m = 0; m < nm && !ovf && !w.sc[SC_ERR]; m++) {
-            const int ms = w.ms[m], ml = w.mlen[m];
+            const int ms = s.ms[m], ml = s.mlen[m];
             for (int i = 0; i < ml; i++) {
-                int p = w.mpool[ms + i], t = typ[p];
+                int p = s.mpool[ms + i], t = typ[p];
                 if (t != 0 && t != 1) activate(p, t, false);
                 else clr(p);
             }
         }
-        const int8_t TT[5] = {0, 2, 3, 4, -1};
         for (int i = 0; i < nq; i++) {
             w.sc[SC_NNEW]++;
             int p = qpos[i];
             if (col[p] == 0 && qcol[i] != 0) w.sc[SC_NZ]++;
             else if (col[p] != 0 && qcol[i] == 0) w.sc[SC_NZ]--;
             col[p] = (int8_t)qcol[i];
-            typ[p] = TT[qname[i]];
+            const int nmq = qname[i];
+            typ[p] = (int8_t)(nmq == M_VLASER ? 2 : nmq == M_HLASER ? 3 : nmq == M_BOMB ? 4 : nmq == M_COOKIE ? -1 : 0);
         }
     }
 
     // ---- combination_match, board.py:600-719
-    __device__ void combination(int p1, int p2) {
+    __device__ __forceinline__ void combination(int p1, int p2) {
         w.sc[SC_NACT] += 2;                                                 // :609
         int t1 = typ[p1], k1 = col[p1], t2 = typ[p2], k2 = col[p2];
         int r1 = p1 / C, c1 = p1 % C, r2 = p2 / C, c2 = p2 % C;
@@ -951,150 +1040,191 @@ struct Serial {
     }
 };
 
+
 // ------------------------------------------------------------------ move()
-// Board.move, board.py:330-395 (the effectiveness test :352 is done by the caller).
-// Returns eliminations; updates the LDS scalars / flags.  Leaves the
-// effective mask of the final board in w.effw.
-template <int MAXN>
-__device__ int board_move(const Params &P, Ws<MAXN> &w, int lane, const LaneJump &J, int p1, int p2,
-                          int &flags) {
+// Board.move, board.py:330-395 (the effectiveness test :352 is done by the
+// caller).  Returns eliminations; leaves the effective mask of the final
+// board in w.effw.
+template <int MAXN, bool GEN>
+__device__ __forceinline__ int board_move(const Params &P, Ws<MAXN, GEN> &w, int lane, const LaneJump &J, Rng &g,
+                          const Cells<MAXN / 64> &cl, int p1, int p2, int &flags, int &nn, int &na) {
     const int N = P.N;
     int8_t *col = w.brd, *typ = w.brd + N;
     int elim = 0;
     if (lane == 0) {                                                        // swap_coords :355
         int8_t x = col[p1]; col[p1] = col[p2]; col[p2] = x;
         x = typ[p1]; typ[p1] = typ[p2]; typ[p2] = x;
-        w.sc[SC_NACT] = 0; w.sc[SC_NNEW] = 0; w.sc[SC_ERR] = 0;
+        w.sc[SC_NACT] = 0; w.sc[SC_NNEW] = 0; w.sc[SC_ERR] = 0; w.sc[SC_A] = 0;
     }
     WSYNC();
     const int t1 = typ[p1], t2 = typ[p2];
-    bool ovf = false;
+    bool ovf = false, err = false;
     if (((t1 != 0 && t1 != 1) && (t2 != 0 && t2 != 1)) || t1 < 0 || t2 < 0) {   // :357-364
         flags |= FL_COMBO;
-        int nz = count_colour_nonzero(P, w, lane);
-        if (lane == 0) {
-            w.sc[SC_NZ] = nz;
-            Serial<MAXN> S(P, w);
-            S.combination(p1, p2);
-            w.sc[SC_A] = S.ovf;
-        }
-        WSYNC();
-        ovf |= w.sc[SC_A] != 0;
-        elim += count_type_zero(P, w, lane);
-        gravity(P, w, lane);
-        refill(P, w, lane, J);
-    }
-    // fast path only when no special can exist on the board
-    bool all_normal = true;
-    for (int p = lane; p < N; p += 64) all_normal &= typ[p] == 1;
-    const bool fast = P.smask == 0 && __ballot(!all_normal) == 0ULL;
-    for (;;) {
-        if (ovf) break;                                          // :367-376
-        if (w.sc[SC_ERR]) break;
-        const int rs = detect_row(P, w, lane);
-        if (rs < 0) break;
-        if (fast) {
-            elim += fast_clear(P, w, lane, rs);
-        } else {
+        if constexpr (GEN) {
             int nz = count_colour_nonzero(P, w, lane);
             if (lane == 0) {
                 w.sc[SC_NZ] = nz;
-                Serial<MAXN> S(P, w);
-                S.build_lines(rs);
-                if (!S.ovf) S.process_lines();
-                if (!S.ovf) S.resolve();
+                Serial<MAXN> S(P, w, w.s);
+                S.combination(p1, p2);
                 w.sc[SC_A] = S.ovf;
             }
             WSYNC();
             ovf |= w.sc[SC_A] != 0;
             elim += count_type_zero(P, w, lane);
+            gravity(P, w, lane);
+            WSYNC();
+            refill(P, w, lane, J, g);
+        } else {
+            err = true;                                                     // lean variant never sees specials
+        }
+    }
+    // wave-parallel cascade only when no special can exist on the board
+    bool fast = !GEN;
+    if (GEN && P.smask == 0) {
+        bool ok = true;
+        for (int p = lane; p < N; p += 64) ok &= typ[p] == 1;
+        fast = __ballot(!ok) == 0ULL;
+    }
+    while (!ovf && !err) {                                                  // :367-376
+        if (w.sc[SC_ERR]) break;
+        Det<MAXN / 64> d;
+        const int rs = detect(P, w, lane, cl, d);
+        if (rs < 0) break;
+        if (fast) {
+            elim += fast_clear(P, w, lane, cl, d, rs);
+        } else {
+            if constexpr (GEN) {
+                int nz = count_colour_nonzero(P, w, lane);
+                if (lane == 0) {
+                    w.sc[SC_NZ] = nz;
+                    Serial<MAXN> S(P, w, w.s);
+                    S.build_lines(rs);
+                    if (!S.ovf) S.process_lines();
+                    if (!S.ovf) S.resolve();
+                    w.sc[SC_A] = S.ovf;
+                }
+                WSYNC();
+                ovf |= w.sc[SC_A] != 0;
+                elim += count_type_zero(P, w, lane);
+            }
         }
         gravity(P, w, lane);
-        refill(P, w, lane, J);
+        WSYNC();
+        refill(P, w, lane, J, g);
     }
-    elim += w.sc[SC_NNEW];                                                  // :378
+    nn = w.sc[SC_NNEW];
+    na = w.sc[SC_NACT];
+    elim += nn;                                                             // :378
     if (ovf) flags |= FL_OVF;
-    if (w.sc[SC_ERR]) flags |= FL_ERR;
-    if (ensure_playable(P, w, lane, J)) flags |= FL_SHUF;                   // :381-391
+    if (err || w.sc[SC_ERR]) flags |= FL_ERR;
+    if (ensure_playable(P, w, lane, J, g, cl)) flags |= FL_SHUF;            // :381-391
     return elim;
 }
 
 // ------------------------------------------------------------------ kernels
-__device__ inline LaneJump load_jump(const Params &P, int lane) {
+__device__ __forceinline__ LaneJump load_jump(const Params &P, int lane, const Rng &g) {
     const uint64_t *t = P.jump + lane * 4;
     LaneJump J;
     J.Aj = U128{t[0], t[1]};
     J.Gj = U128{t[2], t[3]};
+    J.incG = mul128(U128{g.ilo, g.ihi}, J.Gj);
     return J;
 }
 
-template <int MAXN>
+__device__ __forceinline__ Rng load_rng(const uint64_t *p) {
+    Rng g;
+    g.slo = bcast64(p[0]); g.shi = bcast64(p[1]); g.ilo = bcast64(p[2]); g.ihi = bcast64(p[3]); g.h = bcast64(p[4]);
+    return g;
+}
+__device__ __forceinline__ void store_rng(uint64_t *p, const Rng &g, int lane) {
+    if (lane == 0) { p[0] = g.slo; p[1] = g.shi; p[2] = g.ilo; p[3] = g.ihi; p[4] = g.h; }
+}
+
+// TileMatchEnv.step for one env per wave (tile_match_env.py:93-112).
+// GEN=false: lean variant for boards that can hold no special (no specials
+// enabled, cached effective mask trusted).
+template <int MAXN, bool GEN>
 __global__ __launch_bounds__(64 * TMG_WPB) void step_kernel(
     Params P, int64_t n, int8_t *__restrict__ board, uint64_t *__restrict__ rng, int32_t *__restrict__ timer,
     const int32_t *__restrict__ actions, int32_t *__restrict__ reward, int32_t *__restrict__ n_new,
     int32_t *__restrict__ n_act, uint8_t *__restrict__ flags_out, uint64_t *__restrict__ eff, int trust_eff,
     int autoreset) {
-    extern __shared__ __align__(16) unsigned char smem[];
+    TMG_SMEM_DECL(smem);
+    using WS = Ws<MAXN, GEN>;
     const int lane = threadIdx.x & 63;
     const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
-    Ws<MAXN> &w = reinterpret_cast<Ws<MAXN> *>(smem)[wv];
+    WS &w = reinterpret_cast<WS *>(smem)[wv];
     const int64_t e = (int64_t)blockIdx.x * TMG_WPB + wv;
     if (e >= n) return;
 
     const int N = P.N, W = P.W;
-    const int a = actions[e];
-    const int t0 = timer[e];
+    const int a = __builtin_amdgcn_readfirstlane(actions[e]);             // wave-uniform loads
+    const int t0 = __builtin_amdgcn_readfirstlane(timer[e]);
     if (t0 >= P.num_moves || a < 0 || a >= P.A) {                           // tile_match_env.py:94-95
         if (lane == 0) { reward[e] = 0; n_new[e] = 0; n_act[e] = 0; flags_out[e] = FL_ERR; }
         return;
     }
     int8_t *gb = board + e * 2 * N;
     uint64_t *ge = eff + e * W;
+    const int t1 = t0 + 1;
+    const bool done = t1 == P.num_moves;                                    // tile_match_env.py:100-101
+    int flags = done ? FL_DONE : 0;
+    bool effective = false;
+    if (trust_eff) effective = (bcast64(ge[a >> 6]) >> (a & 63)) & 1ULL;    // board.py:352 via cached mask
+    if (trust_eff && !effective && !(done && autoreset)) {                  // no state change at all
+        if (done) for (int i = lane; i < W; i += 64) ge[i] = 0ULL;          // tile_match_env.py:119-120
+        if (lane == 0) { timer[e] = t1; reward[e] = 0; n_new[e] = 0; n_act[e] = 0; flags_out[e] = (uint8_t)flags; }
+        return;
+    }
     int r1, c1, r2, c2;
     action_coords(P.R, P.C, a, r1, c1, r2, c2);
     const int p1 = r1 * P.C + c1, p2 = r2 * P.C + c2;
 
     load_board(P, w, lane, gb);
-    for (int p = lane; p < N; p += 64) w.mark[p] = 0;
+    if constexpr (GEN) {
+        for (int p = lane; p < N; p += 64) w.mark[p] = 0;
+    }
     WSYNC();
-    bool effective;
-    if (trust_eff) {
-        effective = (ge[a >> 6] >> (a & 63)) & 1ULL;                        // board.py:352 via cached mask
-    } else {
-        bool ex = lane == 0 ? eff_exact(P, w, a) : false;
+    if constexpr (!GEN) {                                                   // lean variant precondition
+        bool ok = true;
+        for (int p = lane; p < N; p += 64) ok &= w.brd[N + p] == 1;
+        if (__ballot(!ok) != 0ULL) {
+            if (lane == 0) { reward[e] = 0; n_new[e] = 0; n_act[e] = 0; flags_out[e] = FL_ERR; }
+            return;
+        }
+    }
+    if (!trust_eff) {
+        bool ex = lane == 0 ? eff_exact(P, w.brd, a) : false;
         effective = __ballot(ex) != 0ULL;
     }
-    const int t1 = t0 + 1;
-    const bool done = t1 == P.num_moves;                                    // tile_match_env.py:100-101
-    int flags = done ? FL_DONE : 0;
+    Rng g = load_rng(rng + e * 5);
+    const LaneJump J = load_jump(P, lane, g);
+    const Cells<MAXN / 64> cl = make_cells<MAXN / 64>(P, lane);
     int elim = 0, nn = 0, na = 0;
-    const LaneJump J = load_jump(P, lane);
     bool changed = false;
-    if (lane < 5) w.rng[lane] = rng[e * 5 + lane];
-    WSYNC();
     if (effective) {
-        elim = board_move(P, w, lane, J, p1, p2, flags);
-        nn = w.sc[SC_NNEW];
-        na = w.sc[SC_NACT];
+        elim = board_move(P, w, lane, J, g, cl, p1, p2, flags, nn, na);
         changed = true;
     }
     int tnew = t1;
     if (done && autoreset) {                                                // reset() without a seed
-        generate_board(P, w, lane, J);
+        generate_board(P, w, lane, J, g, cl);
         tnew = 0;
         flags |= FL_RESET;
         changed = true;
     }
     if (changed) {
         store_board(P, w, lane, gb);
-        if (lane < 5) rng[e * 5 + lane] = w.rng[lane];
+        store_rng(rng + e * 5, g, lane);
     }
     if (done && !autoreset) {
         for (int i = lane; i < W; i += 64) ge[i] = 0ULL;                   // tile_match_env.py:119-120
     } else if (changed) {
         for (int i = lane; i < W; i += 64) ge[i] = w.effw[i];
     } else if (!trust_eff) {
-        scan_effective(P, w, lane);
+        scan_effective(P, w, lane, cl, false);
+        WSYNC();
         for (int i = lane; i < W; i += 64) ge[i] = w.effw[i];
     }
     if (lane == 0) {
@@ -1106,41 +1236,47 @@ __global__ __launch_bounds__(64 * TMG_WPB) void step_kernel(
     }
 }
 
+// TileMatchEnv.reset without a seed (tile_match_env.py:84-91)
 template <int MAXN>
 __global__ __launch_bounds__(64 * TMG_WPB) void reset_kernel(Params P, int64_t n, int8_t *__restrict__ board,
                                                              uint64_t *__restrict__ rng, int32_t *__restrict__ timer,
                                                              uint64_t *__restrict__ eff,
                                                              const uint8_t *__restrict__ env_mask) {
-    extern __shared__ __align__(16) unsigned char smem[];
+    TMG_SMEM_DECL(smem);
+    using WS = Ws<MAXN, false>;
     const int lane = threadIdx.x & 63;
     const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
-    Ws<MAXN> &w = reinterpret_cast<Ws<MAXN> *>(smem)[wv];
+    WS &w = reinterpret_cast<WS *>(smem)[wv];
     const int64_t e = (int64_t)blockIdx.x * TMG_WPB + wv;
     if (e >= n) return;
-    if (env_mask && !env_mask[e]) return;
+    if (env_mask && !__builtin_amdgcn_readfirstlane((int)env_mask[e])) return;
     const int N = P.N, W = P.W;
-    const LaneJump J = load_jump(P, lane);
-    if (lane < 5) w.rng[lane] = rng[e * 5 + lane];
-    WSYNC();
-    generate_board(P, w, lane, J);                                          // board.py:95-109
+    Rng g = load_rng(rng + e * 5);
+    const LaneJump J = load_jump(P, lane, g);
+    const Cells<MAXN / 64> cl = make_cells<MAXN / 64>(P, lane);
+    generate_board(P, w, lane, J, g, cl);                                   // board.py:95-109
     store_board(P, w, lane, board + e * 2 * N);
-    if (lane < 5) rng[e * 5 + lane] = w.rng[lane];
+    store_rng(rng + e * 5, g, lane);
     for (int i = lane; i < W; i += 64) eff[e * W + i] = w.effw[i];
     if (lane == 0) timer[e] = 0;
 }
 
+// TileMatchEnv._get_effective_actions for arbitrary boards (tile_match_env.py:118-124)
 template <int MAXN>
 __global__ __launch_bounds__(64 * TMG_WPB) void effective_kernel(Params P, int64_t n, const int8_t *__restrict__ board,
                                                                  uint64_t *__restrict__ eff) {
-    extern __shared__ __align__(16) unsigned char smem[];
+    TMG_SMEM_DECL(smem);
+    using WS = Ws<MAXN, false>;
     const int lane = threadIdx.x & 63;
     const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
-    Ws<MAXN> &w = reinterpret_cast<Ws<MAXN> *>(smem)[wv];
+    WS &w = reinterpret_cast<WS *>(smem)[wv];
     const int64_t e = (int64_t)blockIdx.x * TMG_WPB + wv;
     if (e >= n) return;
     load_board(P, w, lane, board + e * 2 * P.N);
     WSYNC();
-    scan_effective(P, w, lane);
+    const Cells<MAXN / 64> cl = make_cells<MAXN / 64>(P, lane);
+    scan_effective(P, w, lane, cl, false);
+    WSYNC();
     for (int i = lane; i < P.W; i += 64) eff[e * P.W + i] = w.effw[i];
 }
 

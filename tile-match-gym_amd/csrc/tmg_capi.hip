@@ -37,16 +37,23 @@ template <int MAXN>
 static int launch_all(int which, tmg_ctx *ctx, int64_t n, int8_t *board, uint64_t *rng, int32_t *timer,
                       const int32_t *actions, int32_t *reward, int32_t *n_new, int32_t *n_act, uint8_t *flags,
                       uint64_t *eff, const uint8_t *env_mask, int trust_eff, int autoreset, hipStream_t s) {
-    const size_t lds = sizeof(tmg::Ws<MAXN>) * TMG_WPB;
     const dim3 block(64 * TMG_WPB);
     const dim3 grid((unsigned)((n + TMG_WPB - 1) / TMG_WPB));
-    if (which == 0)
-        hipLaunchKernelGGL(tmg::step_kernel<MAXN>, grid, block, lds, s, ctx->P, n, board, rng, timer, actions, reward,
-                           n_new, n_act, flags, eff, trust_eff, autoreset);
-    else if (which == 1)
-        hipLaunchKernelGGL(tmg::reset_kernel<MAXN>, grid, block, lds, s, ctx->P, n, board, rng, timer, eff, env_mask);
-    else
-        hipLaunchKernelGGL(tmg::effective_kernel<MAXN>, grid, block, lds, s, ctx->P, n, (const int8_t *)board, eff);
+    const size_t lean = sizeof(tmg::Ws<MAXN, false>) * TMG_WPB;
+    const size_t gen = sizeof(tmg::Ws<MAXN, true>) * TMG_WPB;
+    if (which == 0) {
+        // lean variant: no special can exist (none enabled) and the cached mask is trusted
+        if (ctx->P.smask == 0 && trust_eff)
+            hipLaunchKernelGGL((tmg::step_kernel<MAXN, false>), grid, block, lean, s, ctx->P, n, board, rng, timer,
+                               actions, reward, n_new, n_act, flags, eff, trust_eff, autoreset);
+        else
+            hipLaunchKernelGGL((tmg::step_kernel<MAXN, true>), grid, block, gen, s, ctx->P, n, board, rng, timer,
+                               actions, reward, n_new, n_act, flags, eff, trust_eff, autoreset);
+    } else if (which == 1) {
+        hipLaunchKernelGGL(tmg::reset_kernel<MAXN>, grid, block, lean, s, ctx->P, n, board, rng, timer, eff, env_mask);
+    } else {
+        hipLaunchKernelGGL(tmg::effective_kernel<MAXN>, grid, block, lean, s, ctx->P, n, (const int8_t *)board, eff);
+    }
     return hip_check(hipGetLastError(), "kernel launch");
 }
 

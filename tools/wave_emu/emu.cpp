@@ -1,0 +1,232 @@
+// Host wave emulator (test/debug tool, never part of the product): runs the
+// kernels of tile-match-gym_amd/csrc/tmg_board.hip with one host thread per
+// lane, so AddressSanitizer / gdb see every LDS and global index.
+#include "hip/hip_runtime.h"
+#include "tmg_board.hip"
+
+#include <setjmp.h>
+#include <ucontext.h>
+
+#include <cstdio>
+#include <dlfcn.h>
+#include <cstring>
+#include <vector>
+
+#if defined(__has_feature)
+#if __has_feature(address_sanitizer)
+#define EMU_ASAN 1
+#endif
+#endif
+#if defined(__SANITIZE_ADDRESS__)
+#define EMU_ASAN 1
+#endif
+#ifdef EMU_ASAN
+#include <sanitizer/common_interface_defs.h>
+#endif
+
+EmuDim emu_block_idx;
+
+namespace {
+constexpr size_t kStack = 1 << 20;
+struct Lane {
+    ucontext_t ctx;                 // only used to enter the fiber the first time
+    jmp_buf jb;                     // later switches: _setjmp/_longjmp (no signal-mask syscalls)
+    std::vector<char> stack;
+    int done = 0, op = 0, arg = 0, started = 0;
+    void *site = nullptr, *site2 = nullptr, *site3 = nullptr;
+    uint64_t val = 0, res = 0;
+};
+Lane g_lanes[64];
+jmp_buf g_main_jb;
+int g_cur = -1;
+unsigned char *g_smem = nullptr;
+void (*g_body)(void *) = nullptr;
+void *g_body_arg = nullptr;
+#ifdef EMU_ASAN
+void *g_main_fake = nullptr;
+const void *g_main_bottom = nullptr;
+size_t g_main_size = 0;
+#endif
+
+void switch_to_lane(int l) {
+    g_cur = l;
+    if (_setjmp(g_main_jb) == 0) {
+#ifdef EMU_ASAN
+        __sanitizer_start_switch_fiber(&g_main_fake, g_lanes[l].stack.data(), kStack);
+#endif
+        if (!g_lanes[l].started) { g_lanes[l].started = 1; setcontext(&g_lanes[l].ctx); }
+        _longjmp(g_lanes[l].jb, 1);
+    }
+#ifdef EMU_ASAN
+    __sanitizer_finish_switch_fiber(g_main_fake, &g_main_bottom, &g_main_size);
+#endif
+}
+void yield_to_main(bool finished) {
+    Lane &L = g_lanes[g_cur];
+#ifdef EMU_ASAN
+    void *fake = nullptr;
+#endif
+    if (finished || _setjmp(L.jb) == 0) {
+#ifdef EMU_ASAN
+        __sanitizer_start_switch_fiber(finished ? nullptr : &fake, g_main_bottom, g_main_size);
+#endif
+        _longjmp(g_main_jb, 1);
+    }
+#ifdef EMU_ASAN
+    __sanitizer_finish_switch_fiber(fake, nullptr, nullptr);
+#endif
+}
+void lane_entry() {
+#ifdef EMU_ASAN
+    __sanitizer_finish_switch_fiber(nullptr, &g_main_bottom, &g_main_size);
+#endif
+    g_body(g_body_arg);
+    g_lanes[g_cur].done = 1;
+    yield_to_main(true);
+}
+}  // namespace
+
+EmuDim emu_thread_idx() { EmuDim d; d.x = (unsigned)g_cur; return d; }
+unsigned char *emu_smem() { return g_smem; }
+
+static void print_site(void *a) {
+    Dl_info di;
+    if (a && dladdr(a, &di) && di.dli_fbase)
+        fprintf(stderr, "%s+0x%lx", di.dli_fname, (unsigned long)((char *)a - (char *)di.dli_fbase));
+    else
+        fprintf(stderr, "%p", a);
+}
+
+__attribute__((noinline)) uint64_t emu_collective(int op, uint64_t v, int arg) {
+    Lane &L = g_lanes[g_cur];
+    L.op = op; L.val = v; L.arg = arg;
+    L.site = __builtin_return_address(0);
+#ifdef EMU_DEEP_SITES
+    L.site2 = __builtin_return_address(1);
+    L.site3 = __builtin_return_address(2);
+#endif
+    yield_to_main(false);
+    return g_lanes[g_cur].res;
+}
+
+// run one workgroup of one wave: every lane to completion, resolving collectives
+static void run_wave(void (*body)(void *), void *arg) {
+    g_body = body; g_body_arg = arg;
+    for (int l = 0; l < 64; l++) {
+        Lane &L = g_lanes[l];
+        if (L.stack.empty()) L.stack.resize(kStack);
+        getcontext(&L.ctx);
+        L.ctx.uc_stack.ss_sp = L.stack.data();
+        L.ctx.uc_stack.ss_size = kStack;
+        L.ctx.uc_link = nullptr;
+        makecontext(&L.ctx, lane_entry, 0);
+        L.done = 0; L.op = 0; L.started = 0;
+    }
+    for (;;) {
+        int live = 0;
+        for (int l = 0; l < 64; l++)
+            if (!g_lanes[l].done) { switch_to_lane(l); }
+        int op = 0;
+        for (int l = 0; l < 64; l++) {
+            if (g_lanes[l].done) continue;
+            live++;
+            if (op == 0) op = g_lanes[l].op;
+            else if (g_lanes[l].op != op) {
+                fprintf(stderr, "wave_emu: divergent collectives (lane %d op %d vs %d) at ", l, g_lanes[l].op, op);
+                print_site(g_lanes[l].site); fprintf(stderr, "\n"); abort();
+            }
+        }
+        if (!live) break;
+        if (live != 64) {
+            fprintf(stderr, "wave_emu: block %u: %d lanes exited before a collective; waiting lanes at:\n",
+                    emu_block_idx.x, 64 - live);
+            for (int l = 0; l < 64; l++) {
+                if (g_lanes[l].done) { fprintf(stderr, "  lane %d: exited\n", l); continue; }
+                fprintf(stderr, "  lane %d: op %d at ", l, g_lanes[l].op); print_site(g_lanes[l].site);
+                fprintf(stderr, " <- "); print_site(g_lanes[l].site2); fprintf(stderr, " <- "); print_site(g_lanes[l].site3);
+                fprintf(stderr, "\n");
+                if (l > 2) break;
+            }
+            abort();
+        }
+        if (op == EMU_BALLOT) {
+            uint64_t m = 0;
+            for (int l = 0; l < 64; l++) m |= (g_lanes[l].val & 1) << l;
+            for (int l = 0; l < 64; l++) g_lanes[l].res = m;
+        } else if (op == EMU_READLANE) {
+            for (int l = 0; l < 64; l++) g_lanes[l].res = g_lanes[g_lanes[l].arg & 63].val;
+        }
+    }
+}
+
+template <class F>
+static void body_thunk(void *p) { (*reinterpret_cast<F *>(p))(); }
+
+template <class F>
+static void run_blocks(int64_t nblocks, size_t lds, F kernel) {
+    for (int64_t b = 0; b < nblocks; b++) {
+        std::vector<unsigned char> smem(lds);          // exactly sized: ASan catches any overrun
+        memset(smem.data(), 0xA5, lds);
+        g_smem = smem.data();
+        emu_block_idx.x = (unsigned)b;
+        run_wave(&body_thunk<F>, &kernel);
+    }
+}
+
+static tmg::Params make_params(int R, int C, int k, int smask, int moves, const uint64_t *jump) {
+    tmg::Params P;
+    P.R = R; P.C = C; P.N = R * C; P.A = 2 * R * C - R - C; P.W = (P.A + 63) / 64;
+    P.k = k; P.smask = smask; P.num_moves = moves;
+    uint32_t rng = (uint32_t)(k - 1), excl = rng + 1;
+    P.thr = rng ? (UINT32_MAX - rng) % excl : 0u;
+    P.jump = jump;
+    return P;
+}
+
+static uint64_t g_jump[256];
+static bool g_jump_init = false;
+
+extern "C" {
+
+int emu_step(int R, int C, int k, int smask, int moves, int64_t n, int8_t *board, uint64_t *rng, int32_t *timer,
+             const int32_t *actions, int32_t *reward, int32_t *n_new, int32_t *n_act, uint8_t *flags, uint64_t *eff,
+             int trust_eff, int autoreset) {
+    if (!g_jump_init) { tmg::build_jump_table(g_jump); g_jump_init = true; }
+    tmg::Params P = make_params(R, C, k, smask, moves, g_jump);
+    const bool lean = smask == 0 && trust_eff;
+    if (P.N <= 128) {
+        if (lean)
+            run_blocks(n, sizeof(tmg::Ws<128, false>), [&] { tmg::step_kernel<128, false>(P, n, board, rng, timer, actions, reward, n_new, n_act, flags, eff, trust_eff, autoreset); });
+        else
+            run_blocks(n, sizeof(tmg::Ws<128, true>), [&] { tmg::step_kernel<128, true>(P, n, board, rng, timer, actions, reward, n_new, n_act, flags, eff, trust_eff, autoreset); });
+    } else {
+        if (lean)
+            run_blocks(n, sizeof(tmg::Ws<512, false>), [&] { tmg::step_kernel<512, false>(P, n, board, rng, timer, actions, reward, n_new, n_act, flags, eff, trust_eff, autoreset); });
+        else
+            run_blocks(n, sizeof(tmg::Ws<512, true>), [&] { tmg::step_kernel<512, true>(P, n, board, rng, timer, actions, reward, n_new, n_act, flags, eff, trust_eff, autoreset); });
+    }
+    return 0;
+}
+
+int emu_reset(int R, int C, int k, int smask, int moves, int64_t n, int8_t *board, uint64_t *rng, int32_t *timer,
+              uint64_t *eff) {
+    if (!g_jump_init) { tmg::build_jump_table(g_jump); g_jump_init = true; }
+    tmg::Params P = make_params(R, C, k, smask, moves, g_jump);
+    if (P.N <= 128)
+        run_blocks(n, sizeof(tmg::Ws<128, false>), [&] { tmg::reset_kernel<128>(P, n, board, rng, timer, eff, nullptr); });
+    else
+        run_blocks(n, sizeof(tmg::Ws<512, false>), [&] { tmg::reset_kernel<512>(P, n, board, rng, timer, eff, nullptr); });
+    return 0;
+}
+
+int emu_effective(int R, int C, int k, int smask, int64_t n, const int8_t *board, uint64_t *eff) {
+    if (!g_jump_init) { tmg::build_jump_table(g_jump); g_jump_init = true; }
+    tmg::Params P = make_params(R, C, k, smask, 1, g_jump);
+    if (P.N <= 128)
+        run_blocks(n, sizeof(tmg::Ws<128, false>), [&] { tmg::effective_kernel<128>(P, n, board, eff); });
+    else
+        run_blocks(n, sizeof(tmg::Ws<512, false>), [&] { tmg::effective_kernel<512>(P, n, board, eff); });
+    return 0;
+}
+
+}  // extern "C"

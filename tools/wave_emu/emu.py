@@ -1,0 +1,85 @@
+"""ctypes driver of the host wave emulator (debug/test tool, not the product).
+
+    LD_PRELOAD=$(gcc -print-file-name=libasan.so) ASAN_OPTIONS=detect_leaks=0 \
+        python tools/wave_emu/emu.py --asan R C k smask n steps
+"""
+import ctypes
+import os
+import sys
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+P = ctypes.c_void_p
+I = ctypes.c_int
+I64 = ctypes.c_int64
+
+
+def load(asan=False):
+    L = ctypes.CDLL(os.path.join(HERE, "libwave_emu_asan.so" if asan else os.environ.get("EMU_LIB", "libwave_emu.so")))
+    L.emu_step.argtypes = [I, I, I, I, I, I64, P, P, P, P, P, P, P, P, P, I, I]
+    L.emu_reset.argtypes = [I, I, I, I, I, I64, P, P, P, P]
+    L.emu_effective.argtypes = [I, I, I, I, I64, P, P]
+    return L
+
+
+class EmuBatch:
+    """Same fields/semantics as oracle.OracleBatch, executed by the emulated kernels."""
+
+    def __init__(self, L, R, C, k, smask, num_moves, rng_words):
+        self.L = L
+        self.R, self.C, self.k, self.smask, self.num_moves = R, C, k, smask, num_moves
+        self.n = rng_words.shape[0]
+        self.A = 2 * R * C - R - C
+        self.W = (self.A + 63) // 64
+        self.board = np.zeros((self.n, 2, R, C), np.int8)
+        self.rng = np.ascontiguousarray(rng_words, dtype=np.uint64).copy()
+        self.timer = np.zeros(self.n, np.int32)
+        self.eff = np.zeros((self.n, self.W), np.uint64)
+        self.reward = np.zeros(self.n, np.int32)
+        self.n_new = np.zeros(self.n, np.int32)
+        self.n_act = np.zeros(self.n, np.int32)
+        self.flags = np.zeros(self.n, np.uint8)
+        self.trust = False
+
+    def reset(self):
+        self.L.emu_reset(self.R, self.C, self.k, self.smask, self.num_moves, self.n, self.board.ctypes.data,
+                         self.rng.ctypes.data, self.timer.ctypes.data, self.eff.ctypes.data)
+        self.trust = True
+
+    def step(self, actions, autoreset=True):
+        a = np.ascontiguousarray(actions, dtype=np.int32)
+        self.L.emu_step(self.R, self.C, self.k, self.smask, self.num_moves, self.n, self.board.ctypes.data,
+                        self.rng.ctypes.data, self.timer.ctypes.data, a.ctypes.data, self.reward.ctypes.data,
+                        self.n_new.ctypes.data, self.n_act.ctypes.data, self.flags.ctypes.data,
+                        self.eff.ctypes.data, int(self.trust), int(autoreset))
+
+
+def main():
+    sys.path[:0] = [ROOT, os.path.join(ROOT, "tile-match-gym_amd")]
+    from oracle import oracle as orc
+    from tile_match_gym_amd.seeding import batch_rng_words
+    args = [a for a in sys.argv[1:] if not a.startswith("--")]
+    R, C, k, sm, n, steps = (int(x) for x in args)
+    L = load(asan="--asan" in sys.argv)
+    w = batch_rng_words(range(100, 100 + n))
+    e = EmuBatch(L, R, C, k, sm, 30, w)
+    o = orc.OracleBatch(R, C, k, sm, 30, w)
+    e.reset(); o.reset()
+    assert np.array_equal(e.board, o.board), "reset board"
+    assert np.array_equal(e.rng, o.rng), "reset rng"
+    assert np.array_equal(e.eff, o.eff), "reset eff"
+    rs = np.random.default_rng(7)
+    for t in range(steps):
+        a = rs.integers(0, e.A, n).astype(np.int32)
+        e.step(a); o.step(a)
+        for name in ("board", "rng", "reward", "n_new", "n_act", "flags", "eff", "timer"):
+            if not np.array_equal(getattr(e, name), getattr(o, name)):
+                bad = np.nonzero((getattr(e, name).reshape(n, -1) != getattr(o, name).reshape(n, -1)).any(1))[0]
+                raise SystemExit(f"step {t}: {name} differs in envs {bad[:10]}")
+    print(f"emu == oracle for {n} envs x {steps} steps ({R}x{C} k={k} smask={sm})")
+
+
+if __name__ == "__main__":
+    main()

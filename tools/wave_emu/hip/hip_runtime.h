@@ -1,0 +1,45 @@
+// Host shim used ONLY by tools/wave_emu: lets csrc/tmg_board.hip compile with
+// g++ so each wavefront runs as 64 user-space fibers (one OS thread), for
+// AddressSanitizer / gdb.  Lanes run one after another between collectives
+// (ballot, readlane, fences/barriers), which are resolved once every lane of
+// the wave has arrived — the lockstep points of the real wavefront.
+#pragma once
+#include <stdint.h>
+#include <cstdlib>
+
+#define __device__
+#define __host__
+#define __global__
+#define __launch_bounds__(...)
+#define __align__(x) alignas(x)
+#define __forceinline__ inline
+#define __shared__
+
+struct EmuDim { unsigned x = 0, y = 0, z = 0; };
+EmuDim emu_thread_idx();
+extern EmuDim emu_block_idx;
+#define threadIdx (emu_thread_idx())
+#define blockIdx (emu_block_idx)
+
+enum EmuOp { EMU_SYNC = 1, EMU_BALLOT = 2, EMU_READLANE = 3 };
+// lane side of a collective: publish (op, value, arg), yield to the scheduler,
+// return the resolved result
+uint64_t emu_collective(int op, uint64_t v, int arg);
+unsigned char *emu_smem();
+
+inline void emu_sync() { emu_collective(EMU_SYNC, 0, 0); }
+inline uint64_t __ballot(int pred) { return emu_collective(EMU_BALLOT, pred ? 1 : 0, 0); }
+inline uint32_t emu_readlane(uint32_t v, int l) { return (uint32_t)emu_collective(EMU_READLANE, v, l); }
+inline uint32_t emu_readfirstlane(uint32_t v) { return emu_readlane(v, 0); }
+inline int emu_readfirstlane(int v) { return (int)emu_readlane((uint32_t)v, 0); }
+#define __builtin_amdgcn_readlane(v, l) emu_readlane((v), (l))
+#define __builtin_amdgcn_readfirstlane(v) emu_readfirstlane(v)
+#define __builtin_amdgcn_fence(order, scope) emu_sync()
+#define __builtin_amdgcn_wave_barrier() ((void)0)
+inline void __syncthreads() { emu_sync(); }
+inline int __popcll(uint64_t x) { return __builtin_popcountll(x); }
+inline int __clzll(uint64_t x) { return x ? __builtin_clzll(x) : 64; }
+inline int __ffsll(unsigned long long x) { return __builtin_ffsll((long long)x); }
+inline uint64_t __umul64hi(uint64_t a, uint64_t b) { return (uint64_t)(((unsigned __int128)a * b) >> 64); }
+
+#define TMG_SMEM_DECL(name) unsigned char *name = emu_smem()
