@@ -51,8 +51,27 @@ enum : int { FL_DONE = 1, FL_COMBO = 2, FL_SHUF = 4, FL_RESET = 8, FL_OVF = 0x40
 struct Params {
     int R, C, N, A, W, k, smask, num_moves;
     uint32_t thr;                 // Lemire threshold (2^32 - k) % k; 0 for powers of two
+    uint32_t cmag, cm1mag;        // ceil(2^20 / C), ceil(2^20 / (C-1)): exact x / C for x < 2^10
     const uint64_t *jump;         // [64][4] jump-ahead table
 };
+
+inline Params make_params(int R, int C, int k, int smask, int num_moves, const uint64_t *jump) {
+    Params P;
+    P.R = R; P.C = C; P.N = R * C;
+    P.A = 2 * R * C - R - C;
+    P.W = (P.A + 63) / 64;
+    P.k = k; P.smask = smask; P.num_moves = num_moves;
+    const uint32_t rng = (uint32_t)(k - 1), excl = rng + 1;
+    P.thr = rng ? (UINT32_MAX - rng) % excl : 0u;
+    P.cmag = ((1u << 20) + (uint32_t)C - 1) / (uint32_t)C;
+    P.cm1mag = C > 1 ? ((1u << 20) + (uint32_t)C - 2) / (uint32_t)(C - 1) : 0u;
+    P.jump = jump;
+    return P;
+}
+
+// x / C and x / (C-1) for 0 <= x < 1024, C <= 64 (error < 2^-10 < 1/C)
+__device__ __forceinline__ int div_c(const Params &P, int x) { return (int)(((uint32_t)x * P.cmag) >> 20); }
+__device__ __forceinline__ int div_cm1(const Params &P, int x) { return (int)(((uint32_t)x * P.cm1mag) >> 20); }
 
 // scalar slots in LDS (lane-0 sections publish through these)
 enum : int { SC_NACT = 0, SC_NNEW, SC_ERR, SC_NZ, SC_A, SC_B, SC_C, SC_D, SC_COUNT = 16 };
@@ -66,6 +85,7 @@ struct WsCore {
     int32_t sc[SC_COUNT];
     int8_t brd[2 * MAXN];          // [colour plane N][type plane N], runtime N (same layout as HBM)
     uint8_t mark[MAXN];
+    alignas(8) int8_t trash[4 * 64];   // target of predicated-off stores (keeps hot loops branch-free)
     union {
         uint32_t draw[MAXN + 128];                  // refill colours
         struct { int8_t tmp[2 * MAXN]; int16_t perm[MAXN]; } sh;   // shuffle
@@ -102,6 +122,13 @@ template <int MAXN>
 struct Ws<MAXN, true> : WsCore<MAXN> {
     WsSerial<MAXN> s;
 };
+
+// Integer predicate helpers: keep per-lane logic in VALU registers (a boolean
+// "&" of two lane compares would be an s_and_b64 on lane masks, i.e. SALU).
+// A predicate is encoded as "zero means true".
+__device__ __forceinline__ uint32_t umin(uint32_t a, uint32_t b) { return a < b ? a : b; }
+__device__ __forceinline__ uint32_t umin3(uint32_t a, uint32_t b, uint32_t c) { return umin(umin(a, b), c); }
+__device__ __forceinline__ uint32_t ne(int a, int b) { return (uint32_t)(a ^ b); }      // 0 iff a == b
 
 __device__ __forceinline__ uint64_t lanemask_lt(int lane) { return lane ? (~0ULL >> (64 - lane)) : 0ULL; }
 
@@ -163,7 +190,8 @@ __device__ __forceinline__ uint32_t r_interval(Rng &g, uint32_t max) {     // ra
 // dst[0..M) <- Generator.integers(1, k+1, M) (board.py:97,129,239), lane-parallel:
 // lane j evaluates PCG output j of the batch by jump-ahead; the caller syncs.
 template <class T>
-__device__ __forceinline__ void draw_colours(const Params &P, int lane, const LaneJump &J, Rng &g, int M, T *dst) {
+__device__ __forceinline__ void draw_colours(const Params &P, int lane, const LaneJump &J, Rng &g, int M, T *dst,
+                                             int8_t *trash) {
     if (M <= 0) return;
     const uint32_t k = (uint32_t)P.k;
     if (k == 1) {                                          // rng == 0: numpy draws nothing
@@ -185,17 +213,14 @@ __device__ __forceinline__ void draw_colours(const Params &P, int lane, const La
     for (int base = 0; base < n64; base += 64) {
         U128 sj = add128(mul128(J.Aj, s), J.incG);
         uint64_t out = xsl_rr(sj);
-        int j = base + lane;
-        if (j < n64) {
-            uint64_t m0 = (uint64_t)(uint32_t)out * k;
-            dst[off + 2 * j] = (T)(1 + (m0 >> 32));
-            rej |= (uint32_t)m0 < P.thr;
-            if (2 * j + 1 < need) {
-                uint64_t m1 = (out >> 32) * k;
-                dst[off + 2 * j + 1] = (T)(1 + (m1 >> 32));
-                rej |= (uint32_t)m1 < P.thr;
-            }
-        }
+        const int j = base + lane;
+        const uint64_t m0 = (uint64_t)(uint32_t)out * k, m1 = (out >> 32) * k;
+        const bool ok0 = j < n64, ok1 = 2 * j + 1 < need;          // ok1 implies ok0
+        T *d0 = ok0 ? dst + off + 2 * j : reinterpret_cast<T *>(trash) + lane;
+        T *d1 = ok1 ? dst + off + 2 * j + 1 : reinterpret_cast<T *>(trash) + lane;
+        *d0 = (T)(1 + (m0 >> 32));
+        *d1 = (T)(1 + (m1 >> 32));
+        rej |= (ok0 & ((uint32_t)m0 < P.thr)) | (ok1 & ((uint32_t)m1 < P.thr));
         int cnt = n64 - base < 64 ? n64 - base : 64;
         s.lo = rdlane64(sj.lo, cnt - 1);
         s.hi = rdlane64(sj.hi, cnt - 1);
@@ -224,11 +249,23 @@ __device__ __forceinline__ void action_coords(int R, int C, int a, int &r1, int 
     if (a < C * (R - 1)) { r1 = a / C; c1 = a % C; r2 = r1 + 1; c2 = c1; }
     else { int i = a - C * (R - 1); r1 = i / (C - 1); c1 = i % (C - 1); r2 = r1; c2 = c1 + 1; }
 }
+// same, branch-free, for lane-parallel scans (a < 2^10)
+__device__ __forceinline__ void action_coords_fast(const Params &P, int a, int &r1, int &c1, int &r2, int &c2) {
+    const int C = P.C, nv = C * (P.R - 1);
+    const bool vert = a < nv;
+    const int i = vert ? a : a - nv;
+    const int q = vert ? div_c(P, i) : div_cm1(P, i);
+    r1 = q;
+    c1 = i - q * (vert ? C : C - 1);
+    r2 = r1 + (vert ? 1 : 0);
+    c2 = c1 + (vert ? 0 : 1);
+}
 
 // per-lane cell coordinates of each 64-cell pass, computed once per kernel
 template <int NP>
 struct Cells {
     int r[NP], c[NP];
+    uint32_t vbad[NP], hbad[NP];   // 0 iff a vertical / horizontal triple can be anchored here
 };
 template <int NP>
 __device__ __forceinline__ Cells<NP> make_cells(const Params &P, int lane) {
@@ -236,8 +273,10 @@ __device__ __forceinline__ Cells<NP> make_cells(const Params &P, int lane) {
 #pragma unroll
     for (int i = 0; i < NP; i++) {
         int p = i * 64 + lane;
-        cl.r[i] = p / P.C;
+        cl.r[i] = div_c(P, p);
         cl.c[i] = p - cl.r[i] * P.C;
+        cl.vbad[i] = (p < P.N && cl.r[i] >= 2) ? 0u : 1u;
+        cl.hbad[i] = (p < P.N && cl.c[i] + 2 < P.C) ? 0u : 1u;
     }
     return cl;
 }
@@ -301,33 +340,37 @@ __device__ __forceinline__ bool eff_exact(const Params &P, const int8_t *brd, in
 
 // Same predicate when the board holds no cookie and no pre-existing colour
 // triple (checked by the caller): only triples through exactly one of the two
-// swapped cells can appear, all inside the reference's window.
-__device__ __forceinline__ bool eff_fast(const Params &P, const int8_t *brd, int a) {
+// swapped cells can appear, all inside the reference's window.  Branch-free:
+// out-of-board neighbours read a clamped cell and are masked to a sentinel.
+__device__ __forceinline__ uint32_t eff_fast(const Params &P, const int8_t *brd, int a) {   // 0 iff effective
     const int R = P.R, C = P.C, N = P.N;
     int r1, c1, r2, c2;
-    action_coords(R, C, a, r1, c1, r2, c2);
+    action_coords_fast(P, a, r1, c1, r2, c2);
     const int8_t *col = brd, *typ = brd + N;
     const int p = r1 * C + c1, q = r2 * C + c2;
-    const int tp = typ[p], tq = typ[q];
-    if ((tp != 0 && tp != 1) && (tq != 0 && tq != 1)) return true;
+    const uint32_t tp = (uint32_t)(int)typ[p], tq = (uint32_t)(int)typ[q];
+    const uint32_t not_both_special = umin(tp, tq) > 1u ? 0u : 1u;    // type not in {0,1} (no cookies here)
     const int x1 = col[p], x2 = col[q];
-    auto eq = [&](int r, int c, int x) -> bool { return r >= 0 && r < R && c >= 0 && c < C && col[r * C + c] == x; };
-    if (r2 == r1 + 1) {       // vertical pair: p (top) receives x2, q (bottom) receives x1
-        if (eq(r1 - 1, c1, x2) && eq(r1 - 2, c1, x2)) return true;
-        if (eq(r1, c1 - 1, x2) && (eq(r1, c1 - 2, x2) || eq(r1, c1 + 1, x2))) return true;
-        if (eq(r1, c1 + 1, x2) && eq(r1, c1 + 2, x2)) return true;
-        if (eq(r2 + 1, c1, x1) && eq(r2 + 2, c1, x1)) return true;
-        if (eq(r2, c1 - 1, x1) && (eq(r2, c1 - 2, x1) || eq(r2, c1 + 1, x1))) return true;
-        if (eq(r2, c1 + 1, x1) && eq(r2, c1 + 2, x1)) return true;
-    } else {                  // horizontal pair: p (left) receives x2, q (right) receives x1
-        if (eq(r1, c1 - 1, x2) && eq(r1, c1 - 2, x2)) return true;
-        if (eq(r1 - 1, c1, x2) && (eq(r1 - 2, c1, x2) || eq(r1 + 1, c1, x2))) return true;
-        if (eq(r1 + 1, c1, x2) && eq(r1 + 2, c1, x2)) return true;
-        if (eq(r1, c2 + 1, x1) && eq(r1, c2 + 2, x1)) return true;
-        if (eq(r1 - 1, c2, x1) && (eq(r1 - 2, c2, x1) || eq(r1 + 1, c2, x1))) return true;
-        if (eq(r1 + 1, c2, x1) && eq(r1 + 2, c2, x1)) return true;
-    }
-    return false;
+    auto at = [&](int r, int c) -> int {        // colour, or -64 outside the board
+        const int oob = r | (R - 1 - r) | c | (C - 1 - c);     // negative iff outside
+        const int v = col[max(min(r, R - 1), 0) * C + max(min(c, C - 1), 0)];
+        return oob < 0 ? -64 : v;
+    };
+    const bool vert = r2 == r1 + 1;
+    const int dr = vert ? 1 : 0, dc = 1 - dr;                 // unit step along the pair
+    const int er = dc, ec = dr;                               // unit step across
+    // p receives x2 (neighbours on p's side), q receives x1 (q's side)
+    const int pa1 = at(r1 - dr, c1 - dc), pa2 = at(r1 - 2 * dr, c1 - 2 * dc);
+    const int qa1 = at(r2 + dr, c2 + dc), qa2 = at(r2 + 2 * dr, c2 + 2 * dc);
+    const int pm1 = at(r1 - er, c1 - ec), pm2 = at(r1 - 2 * er, c1 - 2 * ec);
+    const int pp1 = at(r1 + er, c1 + ec), pp2 = at(r1 + 2 * er, c1 + 2 * ec);
+    const int qm1 = at(r2 - er, c2 - ec), qm2 = at(r2 - 2 * er, c2 - 2 * ec);
+    const int qp1 = at(r2 + er, c2 + ec), qp2 = at(r2 + 2 * er, c2 + 2 * ec);
+    const uint32_t hp = umin3(ne(pa1, x2) | ne(pa2, x2), ne(pm1, x2) | umin(ne(pm2, x2), ne(pp1, x2)),
+                              ne(pp1, x2) | ne(pp2, x2));
+    const uint32_t hq = umin3(ne(qa1, x1) | ne(qa2, x1), ne(qm1, x1) | umin(ne(qm2, x1), ne(qp1, x1)),
+                              ne(qp1, x1) | ne(qp2, x1));
+    return umin3(not_both_special, hp, hq);
 }
 
 // _get_effective_actions / possible_move (tile_match_env.py:118-124, board.py:558-569):
@@ -357,7 +400,8 @@ __device__ __forceinline__ bool scan_effective(const Params &P, WS &w, int lane,
     for (int base = 0, wi = 0; base < P.A; base += 64, wi++) {
         int a = base + lane;
         bool e = false;
-        if (a < P.A) e = exact ? eff_exact(P, w.brd, a) : eff_fast(P, w.brd, a);
+        if (exact) e = a < P.A && eff_exact(P, w.brd, a);
+        else e = (eff_fast(P, w.brd, min(a, P.A - 1)) | (a < P.A ? 0u : 1u)) == 0u;
         uint64_t m = __ballot(e);
         if (lane == 0) w.effw[wi] = m;
         any |= m;
@@ -389,25 +433,26 @@ __device__ __forceinline__ uint64_t bits_at(const uint64_t (&m)[NP], int start, 
 // Returns the bottom-most row holding a line, or -1 (get_colour_lines == []).
 template <class WS>
 __device__ __forceinline__ int detect(const Params &P, const WS &w, int lane, const Cells<WS::NP> &cl, Det<WS::NP> &d) {
-    const int C = P.C, N = P.N;
+    const int C = P.C, N = P.N, N1 = P.N - 1;
     const int8_t *col = w.brd, *typ = w.brd + N;
     int pmax = -1;
 #pragma unroll
     for (int i = 0; i < WS::NP; i++) {
-        int p = i * 64 + lane;
-        bool fv = false, fh = false;
-        if (p < N) {
-            int r = cl.r[i], c = cl.c[i], x = col[p];
-            bool t = typ[p] > 0;
-            fv = t && r >= 2 && col[p - C] == x && col[p - 2 * C] == x;
-            fh = t && c + 2 < C && col[p + 1] == x && col[p + 2] == x;
-        }
-        d.v[i] = __ballot(fv);
-        d.h[i] = __ballot(fh);
-        uint64_t m = d.v[i] | d.h[i];
+        if (i * 64 >= N) { d.v[i] = 0; d.h[i] = 0; continue; }
+        const int p = i * 64 + lane;
+        const int pc = min(p, N1);
+        const int x = col[pc];
+        const int u1 = col[max(pc - C, 0)], u2 = col[max(pc - 2 * C, 0)];
+        const int h1 = col[min(pc + 1, N1)], h2 = col[min(pc + 2, N1)];
+        const uint32_t tbad = (uint32_t)((int)typ[pc] - 1) >> 31;            // 1 iff type <= 0
+        const uint32_t vb = cl.vbad[i] | tbad | ne(u1, x) | ne(u2, x);
+        const uint32_t hb = cl.hbad[i] | tbad | ne(h1, x) | ne(h2, x);
+        d.v[i] = __ballot(vb == 0);
+        d.h[i] = __ballot(hb == 0);
+        const uint64_t m = d.v[i] | d.h[i];
         if (m) pmax = i * 64 + 63 - __clzll(m);
     }
-    return pmax < 0 ? -1 : pmax / C;
+    return pmax < 0 ? -1 : div_c(P, pmax);
 }
 
 // top row of the same-colour run ending at (rs, c) (vertical line start)
@@ -415,8 +460,8 @@ template <class WS>
 __device__ __forceinline__ int run_top(const Params &P, const WS &w, int lane, int rs, int c) {
     const int C = P.C;
     const int x = w.brd[rs * C + c];
-    bool neq = lane < rs && w.brd[lane * C + c] != x;
-    uint64_t mn = __ballot(neq);
+    const int rr = min(lane, rs);
+    uint64_t mn = __ballot(lane < rs ? w.brd[rr * C + c] != x : false);
     return mn ? (63 - __clzll(mn)) + 1 : 0;
 }
 
@@ -448,20 +493,22 @@ __device__ __forceinline__ void gravity(const Params &P, WS &w, int lane) {
     const uint64_t above = lane == 63 ? 0ULL : ~((2ULL << lane) - 1);    // lanes > lane: lower rows
     for (int c0 = 0; c0 < C; c0 += cpp) {
         const int c = c0 + lc;
-        const bool in = lc < cpp && c < C;
-        const int p = r * C + c;
-        int8_t a = 0, t = 0;
-        if (in) { a = col[p]; t = typ[p]; }
-        const bool empty = in && a == 0 && t == 0;
-        const uint64_t E = __ballot(empty);
+        const bool in = (lc < cpp) & (c < C);
+        const int p = in ? r * C + c : 0;
+        const int8_t a = col[p], t = typ[p];
+        const uint32_t occ = in ? (uint32_t)(uint8_t)(a | t) : 1u;            // 0 iff empty cell
+        const uint64_t E = __ballot(occ == 0u);
         if (!E) continue;
         const int below = __popcll(E & colmask & above);
         const int total = __popcll(E & colmask);
+        const bool mv = (in ? umin(occ, (uint32_t)below) : 0u) != 0u;       // non-empty cell that falls
+        const bool clr = (in ? max(total - r, 0) : 0) != 0;                  // top `total` rows become empty
+        const int d = p + below * C;
         WFENCE();
-        if (in) {
-            if (!empty && below) { int d = p + below * C; col[d] = a; typ[d] = t; }
-            if (r < total) { col[p] = 0; typ[p] = 0; }
-        }
+        *(mv ? col + d : w.trash + lane) = a;
+        *(mv ? typ + d : w.trash + 64 + lane) = t;
+        *(clr ? col + p : w.trash + 128 + lane) = 0;
+        *(clr ? typ + p : w.trash + 192 + lane) = 0;
         WFENCE();
     }
 }
@@ -480,17 +527,17 @@ __device__ __forceinline__ void refill(const Params &P, WS &w, int lane, const L
         total += __popcll(E[i]);
     }
     if (total == 0) return;
-    draw_colours(P, lane, J, g, total, w.u.draw);
+    draw_colours(P, lane, J, g, total, w.u.draw, w.trash);
     WSYNC();
     int base = 0;
 #pragma unroll
     for (int i = 0; i < WS::NP; i++) {
-        int p = i * 64 + lane;
-        if ((E[i] >> lane) & 1) {
-            int idx = base + __popcll(E[i] & lanemask_lt(lane));
-            col[p] = (int8_t)w.u.draw[idx];
-            typ[p] = 1;
-        }
+        const int p = i * 64 + lane;
+        const bool e = (E[i] >> lane) & 1;
+        const int idx = base + __popcll(E[i] & lanemask_lt(lane));
+        const int8_t v = (int8_t)w.u.draw[e ? idx : 0];
+        *(e ? col + p : w.trash + lane) = v;
+        *(e ? typ + p : w.trash + 64 + lane) = 1;
         base += __popcll(E[i]);
     }
     WSYNC();
@@ -532,7 +579,7 @@ __device__ __forceinline__ bool ensure_playable(const Params &P, WS &w, int lane
             int r0 = first_line_row(P, w, lane, cl);
             if (r0 < 0) break;
             int row = P.R - 1 < r0 + 1 ? P.R - 1 : r0 + 1;   // colour plane only, rows 0..row
-            draw_colours(P, lane, J, g, (row + 1) * P.C, w.brd);
+            draw_colours(P, lane, J, g, (row + 1) * P.C, w.brd, w.trash);
             WSYNC();
         }
         if (scan_effective(P, w, lane, cl, (P.smask & SP_COOKIE) == 0)) break;
@@ -548,7 +595,7 @@ __device__ __forceinline__ bool ensure_playable(const Params &P, WS &w, int lane
 template <class WS>
 __device__ __forceinline__ void generate_board(const Params &P, WS &w, int lane, const LaneJump &J, Rng &g, const Cells<WS::NP> &cl) {
     const int N = P.N;
-    draw_colours(P, lane, J, g, N, w.brd);
+    draw_colours(P, lane, J, g, N, w.brd, w.trash);
     for (int p = lane; p < N; p += 64) w.brd[N + p] = 1;
     WSYNC();
     ensure_playable(P, w, lane, J, g, cl);

@@ -94,17 +94,8 @@ int tmg_create(tmg_ctx **out, int device, int rows, int cols, int colours, uint3
     if (rc) return rc;
     tmg_ctx *c = new tmg_ctx();
     c->device = device;
+    c->P = tmg::make_params(rows, cols, colours, (int)specials_mask, num_moves, nullptr);
     Params &P = c->P;
-    P.R = rows; P.C = cols; P.N = rows * cols;
-    P.A = 2 * rows * cols - rows - cols;
-    P.W = (P.A + 63) / 64;
-    P.k = colours;
-    P.smask = (int)specials_mask;
-    P.num_moves = num_moves;
-    {
-        uint32_t rng = (uint32_t)(colours - 1), excl = rng + 1;
-        P.thr = rng ? (UINT32_MAX - rng) % excl : 0u;
-    }
     c->maxn = P.N <= 128 ? 128 : 512;
     uint64_t tab[64 * 4];
     tmg::build_jump_table(tab);

@@ -174,13 +174,7 @@ static void run_blocks(int64_t nblocks, size_t lds, F kernel) {
 }
 
 static tmg::Params make_params(int R, int C, int k, int smask, int moves, const uint64_t *jump) {
-    tmg::Params P;
-    P.R = R; P.C = C; P.N = R * C; P.A = 2 * R * C - R - C; P.W = (P.A + 63) / 64;
-    P.k = k; P.smask = smask; P.num_moves = moves;
-    uint32_t rng = (uint32_t)(k - 1), excl = rng + 1;
-    P.thr = rng ? (UINT32_MAX - rng) % excl : 0u;
-    P.jump = jump;
-    return P;
+    return tmg::make_params(R, C, k, smask, moves, jump);
 }
 
 static uint64_t g_jump[256];

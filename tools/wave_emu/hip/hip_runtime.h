@@ -42,4 +42,9 @@ inline int __clzll(uint64_t x) { return x ? __builtin_clzll(x) : 64; }
 inline int __ffsll(unsigned long long x) { return __builtin_ffsll((long long)x); }
 inline uint64_t __umul64hi(uint64_t a, uint64_t b) { return (uint64_t)(((unsigned __int128)a * b) >> 64); }
 
+inline int min(int a, int b) { return a < b ? a : b; }
+inline int max(int a, int b) { return a > b ? a : b; }
+inline unsigned min(unsigned a, unsigned b) { return a < b ? a : b; }
+inline unsigned max(unsigned a, unsigned b) { return a > b ? a : b; }
+
 #define TMG_SMEM_DECL(name) unsigned char *name = emu_smem()
