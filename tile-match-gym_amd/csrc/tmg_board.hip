@@ -25,6 +25,14 @@ namespace tmg {
 #ifndef TMG_WPB
 #define TMG_WPB 1          // waves (boards) per workgroup
 #endif
+#ifndef TMG_WPE
+#define TMG_WPE 0          // minimum waves per SIMD requested from the register allocator (0 = compiler's choice)
+#endif
+#if TMG_WPE > 0
+#define TMG_LAUNCH_BOUNDS __launch_bounds__(64 * TMG_WPB, TMG_WPE)
+#else
+#define TMG_LAUNCH_BOUNDS __launch_bounds__(64 * TMG_WPB)
+#endif
 
 #if TMG_WPB == 1
 #define WSYNC() __syncthreads()
@@ -201,10 +209,11 @@ __device__ __forceinline__ void draw_colours(const Params &P, int lane, const La
     const Rng g0 = g;
     const int off = (int)(g.h >> 32) & 1;
     bool rej = false;
-    if (off && lane == 0) {
-        uint64_t m = (uint64_t)(uint32_t)g.h * k;
-        dst[0] = (T)(1 + (m >> 32));
-        rej |= (uint32_t)m < P.thr;
+    {                                                      // the buffered half-word, if any, is draw 0
+        const uint64_t m = (uint64_t)(uint32_t)g.h * k;
+        const bool st = off & (lane == 0);
+        *(st ? dst : reinterpret_cast<T *>(trash) + lane) = (T)(1 + (m >> 32));
+        rej = st & ((uint32_t)m < P.thr);
     }
     const int need = M - off;
     const int n64 = (need + 1) >> 1;
@@ -226,7 +235,7 @@ __device__ __forceinline__ void draw_colours(const Params &P, int lane, const La
         s.hi = rdlane64(sj.hi, cnt - 1);
         last_hi = rdlane64(out >> 32, cnt - 1);
     }
-    if (__ballot(rej) != 0ULL) {                           // Lemire rejection: exact serial replay
+    if (P.thr != 0u && __ballot(rej) != 0ULL) {            // Lemire rejection: exact serial replay
         WFENCE();
         if (lane == 0) {
             Rng r = g0;
@@ -473,9 +482,20 @@ __device__ __forceinline__ int first_line_row(const Params &P, const WS &w, int 
     Det<WS::NP> d;
     const int rs = detect(P, w, lane, cl, d);
     if (rs < 0) return -1;
-    const uint64_t vb = bits_at(d.v, rs * C, C), hb = bits_at(d.h, rs * C, C);
-    const int c0 = __ffsll((unsigned long long)(vb | hb)) - 1;
-    if (!((vb >> c0) & 1)) return rs;                     // horizontal line at (rs, c0..)
+    // first flagged cell of row rs: lowest pass, then lowest lane
+    int c0 = -1;
+    bool vert = false;
+#pragma unroll
+    for (int i = WS::NP - 1; i >= 0; i--) {
+        if (i * 64 >= P.N) continue;
+        const uint64_t m = __ballot(cl.r[i] == rs) & (d.v[i] | d.h[i]);
+        if (m) {
+            const int b = __ffsll((unsigned long long)m) - 1;
+            c0 = i * 64 + b - rs * C;
+            vert = (d.v[i] >> b) & 1;
+        }
+    }
+    if (!vert) return rs;                                 // horizontal line at (rs, c0..)
     return run_top(P, w, lane, rs, c0);                   // vertical: starts at the top of its run
 }
 
@@ -1192,7 +1212,7 @@ __device__ __forceinline__ void store_rng(uint64_t *p, const Rng &g, int lane) {
 // GEN=false: lean variant for boards that can hold no special (no specials
 // enabled, cached effective mask trusted).
 template <int MAXN, bool GEN>
-__global__ __launch_bounds__(64 * TMG_WPB) void step_kernel(
+__global__ TMG_LAUNCH_BOUNDS void step_kernel(
     Params P, int64_t n, int8_t *__restrict__ board, uint64_t *__restrict__ rng, int32_t *__restrict__ timer,
     const int32_t *__restrict__ actions, int32_t *__restrict__ reward, int32_t *__restrict__ n_new,
     int32_t *__restrict__ n_act, uint8_t *__restrict__ flags_out, uint64_t *__restrict__ eff, int trust_eff,
@@ -1285,7 +1305,7 @@ __global__ __launch_bounds__(64 * TMG_WPB) void step_kernel(
 
 // TileMatchEnv.reset without a seed (tile_match_env.py:84-91)
 template <int MAXN>
-__global__ __launch_bounds__(64 * TMG_WPB) void reset_kernel(Params P, int64_t n, int8_t *__restrict__ board,
+__global__ TMG_LAUNCH_BOUNDS void reset_kernel(Params P, int64_t n, int8_t *__restrict__ board,
                                                              uint64_t *__restrict__ rng, int32_t *__restrict__ timer,
                                                              uint64_t *__restrict__ eff,
                                                              const uint8_t *__restrict__ env_mask) {
@@ -1310,7 +1330,7 @@ __global__ __launch_bounds__(64 * TMG_WPB) void reset_kernel(Params P, int64_t n
 
 // TileMatchEnv._get_effective_actions for arbitrary boards (tile_match_env.py:118-124)
 template <int MAXN>
-__global__ __launch_bounds__(64 * TMG_WPB) void effective_kernel(Params P, int64_t n, const int8_t *__restrict__ board,
+__global__ TMG_LAUNCH_BOUNDS void effective_kernel(Params P, int64_t n, const int8_t *__restrict__ board,
                                                                  uint64_t *__restrict__ eff) {
     TMG_SMEM_DECL(smem);
     using WS = Ws<MAXN, false>;

@@ -11,7 +11,7 @@ import ctypes
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "_lib", "libtmg.so")
+LIB_PATH = os.environ.get("TMG_LIB") or os.path.join(_HERE, "_lib", "libtmg.so")   # TMG_LIB: A/B another build
 EXPORTS = ("tmg_create", "tmg_destroy", "tmg_reset", "tmg_step", "tmg_effective",
            "tmg_num_actions", "tmg_mask_words", "tmg_last_error", "tmg_abi_version")
 ABI_VERSION = 1
