@@ -138,6 +138,19 @@ __device__ __forceinline__ uint32_t umin(uint32_t a, uint32_t b) { return a < b 
 __device__ __forceinline__ uint32_t umin3(uint32_t a, uint32_t b, uint32_t c) { return umin(umin(a, b), c); }
 __device__ __forceinline__ uint32_t ne(int a, int b) { return (uint32_t)(a ^ b); }      // 0 iff a == b
 
+// Wave64 max via DPP (row_shr 1/2/4/8 + row_bcast 15/31, GFX9 encoding): an
+// inclusive scan whose lane 63 holds the maximum; ~7 VALU, no SALU.
+__device__ __forceinline__ int wave_max(int v) {
+    const int lo = (int)0x80000000;
+    v = max(v, __builtin_amdgcn_update_dpp(lo, v, 0x111, 0xf, 0xf, false));
+    v = max(v, __builtin_amdgcn_update_dpp(lo, v, 0x112, 0xf, 0xf, false));
+    v = max(v, __builtin_amdgcn_update_dpp(lo, v, 0x114, 0xf, 0xf, false));
+    v = max(v, __builtin_amdgcn_update_dpp(lo, v, 0x118, 0xf, 0xf, false));
+    v = max(v, __builtin_amdgcn_update_dpp(lo, v, 0x142, 0xa, 0xf, false));
+    v = max(v, __builtin_amdgcn_update_dpp(lo, v, 0x143, 0xc, 0xf, false));
+    return __builtin_amdgcn_readlane(v, 63);
+}
+
 __device__ __forceinline__ uint64_t lanemask_lt(int lane) { return lane ? (~0ULL >> (64 - lane)) : 0ULL; }
 
 __device__ __forceinline__ uint64_t rdlane64(uint64_t v, int l) {
@@ -476,26 +489,34 @@ __device__ __forceinline__ int run_top(const Params &P, const WS &w, int lane, i
 
 // For remove_colour_lines (board.py:120-131): row of the first coord of the
 // first line get_colour_lines would return, or -1 when it returns [].
+// get_colour_lines scans rows bottom-up and, in the first row holding a line,
+// columns left to right with the vertical check first; so the first line is
+// the maximum of key = (row, -col, is_vertical) over anchor cells: one DPP
+// max-reduction instead of mask bookkeeping.
 template <class WS>
 __device__ __forceinline__ int first_line_row(const Params &P, const WS &w, int lane, const Cells<WS::NP> &cl) {
-    const int C = P.C;
-    Det<WS::NP> d;
-    const int rs = detect(P, w, lane, cl, d);
-    if (rs < 0) return -1;
-    // first flagged cell of row rs: lowest pass, then lowest lane
-    int c0 = -1;
-    bool vert = false;
+    const int C = P.C, N = P.N, N1 = P.N - 1;
+    const int8_t *col = w.brd, *typ = w.brd + N;
+    int best = -1;
 #pragma unroll
-    for (int i = WS::NP - 1; i >= 0; i--) {
-        if (i * 64 >= P.N) continue;
-        const uint64_t m = __ballot(cl.r[i] == rs) & (d.v[i] | d.h[i]);
-        if (m) {
-            const int b = __ffsll((unsigned long long)m) - 1;
-            c0 = i * 64 + b - rs * C;
-            vert = (d.v[i] >> b) & 1;
-        }
+    for (int i = 0; i < WS::NP; i++) {
+        if (i * 64 >= N) continue;
+        const int p = i * 64 + lane;
+        const int pc = min(p, N1);
+        const int x = col[pc];
+        const int u1 = col[max(pc - C, 0)], u2 = col[max(pc - 2 * C, 0)];
+        const int h1 = col[min(pc + 1, N1)], h2 = col[min(pc + 2, N1)];
+        const uint32_t tbad = (uint32_t)((int)typ[pc] - 1) >> 31;
+        const uint32_t vb = cl.vbad[i] | tbad | ne(u1, x) | ne(u2, x);
+        const uint32_t hb = cl.hbad[i] | tbad | ne(h1, x) | ne(h2, x);
+        const int base = ((cl.r[i] << 8) | (255 - cl.c[i])) << 1;
+        best = max(best, max(vb == 0 ? base | 1 : -1, hb == 0 ? base : -1));
     }
-    if (!vert) return rs;                                 // horizontal line at (rs, c0..)
+    const int key = wave_max(best);
+    if (key < 0) return -1;
+    const int rs = key >> 9;
+    if (!(key & 1)) return rs;                            // horizontal line at (rs, c0..)
+    const int c0 = 255 - ((key >> 1) & 255);
     return run_top(P, w, lane, rs, c0);                   // vertical: starts at the top of its run
 }
 

@@ -155,6 +155,23 @@ static void run_wave(void (*body)(void *), void *arg) {
             for (int l = 0; l < 64; l++) g_lanes[l].res = m;
         } else if (op == EMU_READLANE) {
             for (int l = 0; l < 64; l++) g_lanes[l].res = g_lanes[g_lanes[l].arg & 63].val;
+        } else if (op == EMU_DPP) {
+            for (int l = 0; l < 64; l++) {
+                const int a = g_lanes[l].arg, ctrl = a & 0xfff, rm = (a >> 12) & 0xf, bm = (a >> 16) & 0xf;
+                const bool bc = (a >> 20) & 1;
+                const uint32_t old = (uint32_t)(g_lanes[l].val >> 32);
+                const int row = l >> 4, bank = (l & 15) >> 2;
+                int srcl = -1;
+                if (ctrl >= 0x111 && ctrl <= 0x11f) { int n = ctrl - 0x110; if ((l & 15) >= n) srcl = l - n; }
+                else if (ctrl == 0x142) { if (row >= 1) srcl = row * 16 - 1; }
+                else if (ctrl == 0x143) { if (row >= 2) srcl = 31; }
+                else { fprintf(stderr, "wave_emu: unsupported DPP ctrl 0x%x\n", ctrl); abort(); }
+                uint32_t r;
+                if (!((rm >> row) & 1) || !((bm >> bank) & 1)) r = old;
+                else if (srcl < 0) r = bc ? 0u : old;
+                else r = (uint32_t)g_lanes[srcl].val;
+                g_lanes[l].res = r;
+            }
         }
     }
 }

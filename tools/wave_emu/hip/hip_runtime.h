@@ -21,7 +21,7 @@ extern EmuDim emu_block_idx;
 #define threadIdx (emu_thread_idx())
 #define blockIdx (emu_block_idx)
 
-enum EmuOp { EMU_SYNC = 1, EMU_BALLOT = 2, EMU_READLANE = 3 };
+enum EmuOp { EMU_SYNC = 1, EMU_BALLOT = 2, EMU_READLANE = 3, EMU_DPP = 4 };
 // lane side of a collective: publish (op, value, arg), yield to the scheduler,
 // return the resolved result
 uint64_t emu_collective(int op, uint64_t v, int arg);
@@ -32,6 +32,12 @@ inline uint64_t __ballot(int pred) { return emu_collective(EMU_BALLOT, pred ? 1 
 inline uint32_t emu_readlane(uint32_t v, int l) { return (uint32_t)emu_collective(EMU_READLANE, v, l); }
 inline uint32_t emu_readfirstlane(uint32_t v) { return emu_readlane(v, 0); }
 inline int emu_readfirstlane(int v) { return (int)emu_readlane((uint32_t)v, 0); }
+// DPP: arg packs ctrl | row_mask << 12 | bank_mask << 16 | bound_ctrl << 20; value packs old << 32 | src
+inline int emu_update_dpp(int old, int src, int ctrl, int row_mask, int bank_mask, bool bound_ctrl) {
+    uint64_t v = ((uint64_t)(uint32_t)old << 32) | (uint32_t)src;
+    return (int)(uint32_t)emu_collective(EMU_DPP, v, ctrl | (row_mask << 12) | (bank_mask << 16) | ((bound_ctrl ? 1 : 0) << 20));
+}
+#define __builtin_amdgcn_update_dpp(o, s, c, r, b, bc) emu_update_dpp((o), (s), (c), (r), (b), (bc))
 #define __builtin_amdgcn_readlane(v, l) emu_readlane((v), (l))
 #define __builtin_amdgcn_readfirstlane(v) emu_readfirstlane(v)
 #define __builtin_amdgcn_fence(order, scope) emu_sync()
