@@ -24,7 +24,7 @@
 #include <sanitizer/common_interface_defs.h>
 #endif
 
-EmuDim emu_block_idx;
+EmuDim emu_block_idx, emu_grid_dim;
 
 namespace {
 constexpr size_t kStack = 1 << 20;
@@ -180,7 +180,12 @@ template <class F>
 static void body_thunk(void *p) { (*reinterpret_cast<F *>(p))(); }
 
 template <class F>
-static void run_blocks(int64_t nblocks, size_t lds, F kernel) {
+static void run_blocks(int64_t n, size_t lds, F kernel) {
+    // one wave per block; EMU_EPW > 1 exercises the kernels' grid-stride env loop
+    int epw = 1;
+    if (const char *v = getenv("EMU_EPW")) epw = atoi(v) > 0 ? atoi(v) : 1;
+    const int64_t nblocks = (n + epw - 1) / epw;
+    emu_grid_dim.x = (unsigned)nblocks;
     for (int64_t b = 0; b < nblocks; b++) {
         std::vector<unsigned char> smem(lds);          // exactly sized: ASan catches any overrun
         memset(smem.data(), 0xA5, lds);

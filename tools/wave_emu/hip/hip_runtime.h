@@ -17,9 +17,10 @@
 
 struct EmuDim { unsigned x = 0, y = 0, z = 0; };
 EmuDim emu_thread_idx();
-extern EmuDim emu_block_idx;
+extern EmuDim emu_block_idx, emu_grid_dim;
 #define threadIdx (emu_thread_idx())
 #define blockIdx (emu_block_idx)
+#define gridDim (emu_grid_dim)
 
 enum EmuOp { EMU_SYNC = 1, EMU_BALLOT = 2, EMU_READLANE = 3, EMU_DPP = 4 };
 // lane side of a collective: publish (op, value, arg), yield to the scheduler,
