@@ -1211,12 +1211,12 @@ __device__ __forceinline__ int board_move(const Params &P, Ws<MAXN, GEN> &w, int
 }
 
 // ------------------------------------------------------------------ kernels
-__device__ __forceinline__ LaneJump load_jump(const Params &P, int lane) {
+__device__ __forceinline__ LaneJump load_jump(const Params &P, int lane, const Rng &g) {
     const uint64_t *t = P.jump + lane * 4;
     LaneJump J;
     J.Aj = U128{t[0], t[1]};
     J.Gj = U128{t[2], t[3]};
-    J.incG = U128{0, 0};
+    J.incG = mul128(U128{g.ilo, g.ihi}, J.Gj);
     return J;
 }
 
@@ -1229,17 +1229,23 @@ __device__ __forceinline__ void store_rng(uint64_t *p, const Rng &g, int lane) {
     if (lane == 0) { p[0] = g.slo; p[1] = g.shi; p[2] = g.ilo; p[3] = g.ihi; p[4] = g.h; }
 }
 
-// TileMatchEnv.step for one env (tile_match_env.py:93-112), executed by one wave.
+// TileMatchEnv.step for one env per wave (tile_match_env.py:93-112).
 // GEN=false: lean variant for boards that can hold no special (no specials
 // enabled, cached effective mask trusted).
 template <int MAXN, bool GEN>
-__device__ __forceinline__ void step_env(const Params &P, Ws<MAXN, GEN> &w, int lane, const LaneJump &J0,
-                                         const Cells<MAXN / 64> &cl, int64_t e, int8_t *__restrict__ board,
-                                         uint64_t *__restrict__ rng, int32_t *__restrict__ timer,
-                                         const int32_t *__restrict__ actions, int32_t *__restrict__ reward,
-                                         int32_t *__restrict__ n_new, int32_t *__restrict__ n_act,
-                                         uint8_t *__restrict__ flags_out, uint64_t *__restrict__ eff, int trust_eff,
-                                         int autoreset) {
+__global__ TMG_LAUNCH_BOUNDS void step_kernel(
+    Params P, int64_t n, int8_t *__restrict__ board, uint64_t *__restrict__ rng, int32_t *__restrict__ timer,
+    const int32_t *__restrict__ actions, int32_t *__restrict__ reward, int32_t *__restrict__ n_new,
+    int32_t *__restrict__ n_act, uint8_t *__restrict__ flags_out, uint64_t *__restrict__ eff, int trust_eff,
+    int autoreset) {
+    TMG_SMEM_DECL(smem);
+    using WS = Ws<MAXN, GEN>;
+    const int lane = threadIdx.x & 63;
+    const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    WS &w = reinterpret_cast<WS *>(smem)[wv];
+    const int64_t e = (int64_t)blockIdx.x * TMG_WPB + wv;
+    if (e >= n) return;
+
     const int N = P.N, W = P.W;
     const int a = __builtin_amdgcn_readfirstlane(actions[e]);             // wave-uniform loads
     const int t0 = __builtin_amdgcn_readfirstlane(timer[e]);
@@ -1263,7 +1269,6 @@ __device__ __forceinline__ void step_env(const Params &P, Ws<MAXN, GEN> &w, int 
     action_coords(P.R, P.C, a, r1, c1, r2, c2);
     const int p1 = r1 * P.C + c1, p2 = r2 * P.C + c2;
 
-    WSYNC();                                                                // previous env's LDS reads done
     load_board(P, w, lane, gb);
     if constexpr (GEN) {
         for (int p = lane; p < N; p += 64) w.mark[p] = 0;
@@ -1282,8 +1287,8 @@ __device__ __forceinline__ void step_env(const Params &P, Ws<MAXN, GEN> &w, int 
         effective = __ballot(ex) != 0ULL;
     }
     Rng g = load_rng(rng + e * 5);
-    LaneJump J = J0;
-    J.incG = mul128(U128{g.ilo, g.ihi}, J.Gj);
+    const LaneJump J = load_jump(P, lane, g);
+    const Cells<MAXN / 64> cl = make_cells<MAXN / 64>(P, lane);
     int elim = 0, nn = 0, na = 0;
     bool changed = false;
     if (effective) {
@@ -1319,80 +1324,48 @@ __device__ __forceinline__ void step_env(const Params &P, Ws<MAXN, GEN> &w, int 
     }
 }
 
-// Each wave steps `epw` envs (grid-stride), so a launch is a few thousand
-// workgroups rather than one per env; per-wave setup is hoisted.
-template <int MAXN, bool GEN>
-__global__ TMG_LAUNCH_BOUNDS void step_kernel(
-    Params P, int64_t n, int8_t *__restrict__ board, uint64_t *__restrict__ rng, int32_t *__restrict__ timer,
-    const int32_t *__restrict__ actions, int32_t *__restrict__ reward, int32_t *__restrict__ n_new,
-    int32_t *__restrict__ n_act, uint8_t *__restrict__ flags_out, uint64_t *__restrict__ eff, int trust_eff,
-    int autoreset) {
-    TMG_SMEM_DECL(smem);
-    using WS = Ws<MAXN, GEN>;
-    const int lane = threadIdx.x & 63;
-    const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
-    WS &w = reinterpret_cast<WS *>(smem)[wv];
-    const int64_t stride = (int64_t)gridDim.x * TMG_WPB;
-    int64_t e = (int64_t)blockIdx.x * TMG_WPB + wv;
-    if (e >= n) return;
-    const LaneJump J = load_jump(P, lane);
-    const Cells<MAXN / 64> cl = make_cells<MAXN / 64>(P, lane);
-    for (; e < n; e += stride)
-        step_env<MAXN, GEN>(P, w, lane, J, cl, e, board, rng, timer, actions, reward, n_new, n_act, flags_out, eff,
-                            trust_eff, autoreset);
-}
-
 // TileMatchEnv.reset without a seed (tile_match_env.py:84-91)
 template <int MAXN>
 __global__ TMG_LAUNCH_BOUNDS void reset_kernel(Params P, int64_t n, int8_t *__restrict__ board,
-                                               uint64_t *__restrict__ rng, int32_t *__restrict__ timer,
-                                               uint64_t *__restrict__ eff, const uint8_t *__restrict__ env_mask) {
+                                                             uint64_t *__restrict__ rng, int32_t *__restrict__ timer,
+                                                             uint64_t *__restrict__ eff,
+                                                             const uint8_t *__restrict__ env_mask) {
     TMG_SMEM_DECL(smem);
     using WS = Ws<MAXN, false>;
     const int lane = threadIdx.x & 63;
     const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
     WS &w = reinterpret_cast<WS *>(smem)[wv];
-    const int64_t stride = (int64_t)gridDim.x * TMG_WPB;
-    int64_t e = (int64_t)blockIdx.x * TMG_WPB + wv;
+    const int64_t e = (int64_t)blockIdx.x * TMG_WPB + wv;
     if (e >= n) return;
+    if (env_mask && !__builtin_amdgcn_readfirstlane((int)env_mask[e])) return;
     const int N = P.N, W = P.W;
-    const LaneJump J0 = load_jump(P, lane);
+    Rng g = load_rng(rng + e * 5);
+    const LaneJump J = load_jump(P, lane, g);
     const Cells<MAXN / 64> cl = make_cells<MAXN / 64>(P, lane);
-    for (; e < n; e += stride) {
-        if (env_mask && !__builtin_amdgcn_readfirstlane((int)env_mask[e])) continue;
-        Rng g = load_rng(rng + e * 5);
-        LaneJump J = J0;
-        J.incG = mul128(U128{g.ilo, g.ihi}, J.Gj);
-        WSYNC();
-        generate_board(P, w, lane, J, g, cl);                               // board.py:95-109
-        store_board(P, w, lane, board + e * 2 * N);
-        store_rng(rng + e * 5, g, lane);
-        for (int i = lane; i < W; i += 64) eff[e * W + i] = w.effw[i];
-        if (lane == 0) timer[e] = 0;
-    }
+    generate_board(P, w, lane, J, g, cl);                                   // board.py:95-109
+    store_board(P, w, lane, board + e * 2 * N);
+    store_rng(rng + e * 5, g, lane);
+    for (int i = lane; i < W; i += 64) eff[e * W + i] = w.effw[i];
+    if (lane == 0) timer[e] = 0;
 }
 
 // TileMatchEnv._get_effective_actions for arbitrary boards (tile_match_env.py:118-124)
 template <int MAXN>
 __global__ TMG_LAUNCH_BOUNDS void effective_kernel(Params P, int64_t n, const int8_t *__restrict__ board,
-                                                   uint64_t *__restrict__ eff) {
+                                                                 uint64_t *__restrict__ eff) {
     TMG_SMEM_DECL(smem);
     using WS = Ws<MAXN, false>;
     const int lane = threadIdx.x & 63;
     const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
     WS &w = reinterpret_cast<WS *>(smem)[wv];
-    const int64_t stride = (int64_t)gridDim.x * TMG_WPB;
-    int64_t e = (int64_t)blockIdx.x * TMG_WPB + wv;
+    const int64_t e = (int64_t)blockIdx.x * TMG_WPB + wv;
     if (e >= n) return;
+    load_board(P, w, lane, board + e * 2 * P.N);
+    WSYNC();
     const Cells<MAXN / 64> cl = make_cells<MAXN / 64>(P, lane);
-    for (; e < n; e += stride) {
-        WSYNC();
-        load_board(P, w, lane, board + e * 2 * P.N);
-        WSYNC();
-        scan_effective(P, w, lane, cl, false);
-        WSYNC();
-        for (int i = lane; i < P.W; i += 64) eff[e * P.W + i] = w.effw[i];
-    }
+    scan_effective(P, w, lane, cl, false);
+    WSYNC();
+    for (int i = lane; i < P.W; i += 64) eff[e * P.W + i] = w.effw[i];
 }
 
 }  // namespace tmg

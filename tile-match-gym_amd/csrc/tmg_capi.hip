@@ -2,7 +2,6 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
-#include <cstdlib>
 #include <cstring>
 #include <string>
 
@@ -30,7 +29,6 @@ struct tmg_ctx {
     tmg::Params P;
     uint64_t *d_jump;
     int maxn;
-    int epw;       // envs per wave (grid-stride); TMG_EPW env var overrides
 };
 
 using tmg::Params;
@@ -40,8 +38,7 @@ static int launch_all(int which, tmg_ctx *ctx, int64_t n, int8_t *board, uint64_
                       const int32_t *actions, int32_t *reward, int32_t *n_new, int32_t *n_act, uint8_t *flags,
                       uint64_t *eff, const uint8_t *env_mask, int trust_eff, int autoreset, hipStream_t s) {
     const dim3 block(64 * TMG_WPB);
-    const int64_t waves = (n + ctx->epw - 1) / ctx->epw;                  // each wave steps up to epw envs
-    const dim3 grid((unsigned)((waves + TMG_WPB - 1) / TMG_WPB));
+    const dim3 grid((unsigned)((n + TMG_WPB - 1) / TMG_WPB));
     const size_t lean = sizeof(tmg::Ws<MAXN, false>) * TMG_WPB;
     const size_t gen = sizeof(tmg::Ws<MAXN, true>) * TMG_WPB;
     if (which == 0) {
@@ -100,8 +97,6 @@ int tmg_create(tmg_ctx **out, int device, int rows, int cols, int colours, uint3
     c->P = tmg::make_params(rows, cols, colours, (int)specials_mask, num_moves, nullptr);
     Params &P = c->P;
     c->maxn = P.N <= 128 ? 128 : 512;
-    c->epw = 8;
-    if (const char *v = getenv("TMG_EPW")) { int x = atoi(v); if (x >= 1 && x <= 4096) c->epw = x; }
     uint64_t tab[64 * 4];
     tmg::build_jump_table(tab);
     rc = hip_check(hipMalloc(&c->d_jump, sizeof tab), "hipMalloc");
