@@ -49,7 +49,6 @@ class _EmuBackend:
 @pytest.mark.parametrize("autoreset", [False, True])
 def test_trajectory_golden_emulated(emu_lib, name, autoreset, monkeypatch):
     emu, L = emu_lib
-    # autoreset runs also exercise the kernels' multi-env-per-wave loop
-    monkeypatch.setenv("EMU_EPW", "3" if autoreset else "1")
+    monkeypatch.setenv("EMU_EPW", "1")      # one env per workgroup, as libtmg launches
     d = load_traj(name)
     assert replay_trajectory(d, _EmuBackend(emu, L, d), autoreset) > 0
