@@ -81,6 +81,27 @@ inline Params make_params(int R, int C, int k, int smask, int num_moves, const u
 __device__ __forceinline__ int div_c(const Params &P, int x) { return (int)(((uint32_t)x * P.cmag) >> 20); }
 __device__ __forceinline__ int div_cm1(const Params &P, int x) { return (int)(((uint32_t)x * P.cm1mag) >> 20); }
 
+// Diagnostic build only (TMG_STAMPS=1, never the product library): lane 0
+// records s_memrealtime (100 MHz) at phase boundaries of every env.
+#ifndef TMG_STAMPS
+#define TMG_STAMPS 0
+#endif
+#if TMG_STAMPS
+constexpr int kStampEnvs = 1 << 18, kStampSlots = 8;
+__device__ uint64_t g_stamps[kStampEnvs * kStampSlots];
+#define STAMP(e, slot)                                                                           \
+    do {                                                                                         \
+        if (lane == 0 && (e) < kStampEnvs) g_stamps[(e) * kStampSlots + (slot)] = __builtin_amdgcn_s_memrealtime(); \
+    } while (0)
+#define STAMPV(e, slot, v)                                                                       \
+    do {                                                                                         \
+        if (lane == 0 && (e) < kStampEnvs) g_stamps[(e) * kStampSlots + (slot)] = (uint64_t)(v); \
+    } while (0)
+#else
+#define STAMP(e, slot) ((void)0)
+#define STAMPV(e, slot, v) ((void)0)
+#endif
+
 // scalar slots in LDS (lane-0 sections publish through these)
 enum : int { SC_NACT = 0, SC_NNEW, SC_ERR, SC_NZ, SC_A, SC_B, SC_C, SC_D, SC_COUNT = 16 };
 
@@ -1135,7 +1156,7 @@ struct Serial {
 // board in w.effw.
 template <int MAXN, bool GEN>
 __device__ __forceinline__ int board_move(const Params &P, Ws<MAXN, GEN> &w, int lane, const LaneJump &J, Rng &g,
-                          const Cells<MAXN / 64> &cl, int p1, int p2, int &flags, int &nn, int &na) {
+                          const Cells<MAXN / 64> &cl, int p1, int p2, int &flags, int &nn, int &na, int64_t e) {
     const int N = P.N;
     int8_t *col = w.brd, *typ = w.brd + N;
     int elim = 0;
@@ -1174,6 +1195,8 @@ __device__ __forceinline__ int board_move(const Params &P, Ws<MAXN, GEN> &w, int
         for (int p = lane; p < N; p += 64) ok &= typ[p] == 1;
         fast = __ballot(!ok) == 0ULL;
     }
+    int iters = 0;
+    (void)e;
     while (!ovf && !err) {                                                  // :367-376
         if (w.sc[SC_ERR]) break;
         Det<MAXN / 64> d;
@@ -1200,13 +1223,18 @@ __device__ __forceinline__ int board_move(const Params &P, Ws<MAXN, GEN> &w, int
         gravity(P, w, lane);
         WSYNC();
         refill(P, w, lane, J, g);
+        iters++;
     }
+    STAMP(e, 2);
+    STAMPV(e, 6, iters);
+    (void)iters;
     nn = w.sc[SC_NNEW];
     na = w.sc[SC_NACT];
     elim += nn;                                                             // :378
     if (ovf) flags |= FL_OVF;
     if (err || w.sc[SC_ERR]) flags |= FL_ERR;
     if (ensure_playable(P, w, lane, J, g, cl)) flags |= FL_SHUF;            // :381-391
+    STAMP(e, 3);
     return elim;
 }
 
@@ -1247,6 +1275,7 @@ __global__ TMG_LAUNCH_BOUNDS void step_kernel(
     if (e >= n) return;
 
     const int N = P.N, W = P.W;
+    STAMP(e, 0);
     const int a = __builtin_amdgcn_readfirstlane(actions[e]);             // wave-uniform loads
     const int t0 = __builtin_amdgcn_readfirstlane(timer[e]);
     if (t0 >= P.num_moves || a < 0 || a >= P.A) {                           // tile_match_env.py:94-95
@@ -1263,6 +1292,7 @@ __global__ TMG_LAUNCH_BOUNDS void step_kernel(
     if (trust_eff && !effective && !(done && autoreset)) {                  // no state change at all
         if (done) for (int i = lane; i < W; i += 64) ge[i] = 0ULL;          // tile_match_env.py:119-120
         if (lane == 0) { timer[e] = t1; reward[e] = 0; n_new[e] = 0; n_act[e] = 0; flags_out[e] = (uint8_t)flags; }
+        STAMP(e, 7);
         return;
     }
     int r1, c1, r2, c2;
@@ -1291,10 +1321,12 @@ __global__ TMG_LAUNCH_BOUNDS void step_kernel(
     const Cells<MAXN / 64> cl = make_cells<MAXN / 64>(P, lane);
     int elim = 0, nn = 0, na = 0;
     bool changed = false;
+    STAMP(e, 1);
     if (effective) {
-        elim = board_move(P, w, lane, J, g, cl, p1, p2, flags, nn, na);
+        elim = board_move(P, w, lane, J, g, cl, p1, p2, flags, nn, na, e);
         changed = true;
     }
+    STAMP(e, 4);
     int tnew = t1;
     if (done && autoreset) {                                                // reset() without a seed
         generate_board(P, w, lane, J, g, cl);
@@ -1302,6 +1334,7 @@ __global__ TMG_LAUNCH_BOUNDS void step_kernel(
         flags |= FL_RESET;
         changed = true;
     }
+    STAMP(e, 5);
     if (changed) {
         store_board(P, w, lane, gb);
         store_rng(rng + e * 5, g, lane);
@@ -1322,6 +1355,7 @@ __global__ TMG_LAUNCH_BOUNDS void step_kernel(
         n_act[e] = na;
         flags_out[e] = (uint8_t)flags;
     }
+    STAMP(e, 7);
 }
 
 // TileMatchEnv.reset without a seed (tile_match_env.py:84-91)

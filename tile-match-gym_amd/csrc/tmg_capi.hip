@@ -137,6 +137,15 @@ int tmg_effective(tmg_ctx *ctx, int64_t n, const int8_t *board, uint64_t *eff, v
                     nullptr, eff, nullptr, 0, 0, stream);
 }
 
+#if TMG_STAMPS
+// diagnostic build only: copy the per-env phase stamps (uint64 [n][8]) to host memory
+__attribute__((visibility("default"))) int tmg_debug_stamps(uint64_t *host, int64_t n) {
+    if (n > tmg::kStampEnvs) n = tmg::kStampEnvs;
+    return hip_check(hipMemcpyFromSymbol(host, HIP_SYMBOL(tmg::g_stamps), (size_t)n * tmg::kStampSlots * sizeof(uint64_t), 0,
+                                         hipMemcpyDeviceToHost), "hipMemcpyFromSymbol");
+}
+#endif
+
 int tmg_num_actions(const tmg_ctx *ctx) { return ctx ? ctx->P.A : -1; }
 int tmg_mask_words(const tmg_ctx *ctx) { return ctx ? ctx->P.W : -1; }
 const char *tmg_last_error(void) { return g_err.c_str(); }

@@ -54,4 +54,6 @@ inline int max(int a, int b) { return a > b ? a : b; }
 inline unsigned min(unsigned a, unsigned b) { return a < b ? a : b; }
 inline unsigned max(unsigned a, unsigned b) { return a > b ? a : b; }
 
+inline uint64_t __builtin_amdgcn_s_memrealtime() { return 0; }
+
 #define TMG_SMEM_DECL(name) unsigned char *name = emu_smem()
