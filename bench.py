@@ -56,14 +56,14 @@ def cpu_baseline(R, C, k, smask, moves, budget_s=12.0):
     n = 2048
     o = orc.OracleBatch(R, C, k, smask, moves, batch_rng_words(range(n)), threads=threads)
     o.reset()
-    A = 2 * R * C - R - C
-    rs = np.random.default_rng(12345)
-    acts = rs.integers(0, A, (moves, n)).astype(np.int32)
+    from tile_match_gym_amd.shard import synthetic_actions
+    T = 300
+    acts = synthetic_actions(range(n), T, 2 * R * C - R - C)
     steps = 0
     t0 = time.perf_counter()
     while True:
         for t in range(moves):
-            o.step(acts[t], autoreset=True)
+            o.step(acts[(steps + t) % T], autoreset=True)
         steps += moves
         el = time.perf_counter() - t0
         if el >= budget_s:
@@ -94,9 +94,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    from tile_match_gym_amd.shard import dist_env, max_over_ranks, shard_range, shard_seeds, synthetic_actions
+    world, rank, local_rank = dist_env()
     dist = None
     if world > 1:
         import torch.distributed as dist
@@ -111,11 +110,10 @@ def main():
     if args.boards:
         nb = args.boards
     moves = 30
-    env = TileMatchVecEnv(nb, R, C, k, moves, cl, co, seeds=range(rank * nb, (rank + 1) * nb), device=dev,
-                          autoreset=True)
+    env = TileMatchVecEnv(nb, R, C, k, moves, cl, co, seeds=shard_seeds(rank, nb), device=dev, autoreset=True)
     A = env.num_actions
     T = 300
-    acts = torch.from_numpy(np.random.default_rng(12345 + rank).integers(0, A, (T, nb)).astype(np.int32)).to(dev)
+    acts = torch.from_numpy(synthetic_actions(shard_range(rank, nb), T, A)).to(dev)
     env.reset()
     for t in range(args.warmup):
         env.step_raw(acts[t % T])
@@ -138,13 +136,8 @@ def main():
     kern_ms = sum(a.elapsed_time(b) for a, b in ev) / max(1, args.steps)
     flags = env.flags.cpu().numpy()
     assert not (flags & 0xC0).any(), "error/overflow flag raised during the bench"
-    if dist:
-        tt = torch.tensor([el], dtype=torch.float64, device=dev)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        el = float(tt.item())
-        kk = torch.tensor([kern_ms], dtype=torch.float64, device=dev)
-        dist.all_reduce(kk, op=dist.ReduceOp.MAX)
-        kern_ms = float(kk.item())
+    el = max_over_ranks(el, dist, dev)
+    kern_ms = max_over_ranks(kern_ms, dist, dev)
 
     if rank == 0:
         total = nb * world * args.steps
@@ -166,7 +159,7 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "int8",
-            "data": "synthetic (uniform random actions from default_rng(12345); seeds = global env index)",
+            "data": "synthetic (uniform random actions, counter-based per (step, global env); seeds = global env index)",
             "config": {"workload": f"{args.config}: {desc}, num_moves=30, autoreset",
                        "boards_per_gpu": nb, "rows": R, "cols": C, "colours": k,
                        "specials": cl + co, "parallelism": f"dp{world} (independent env shards, no collective)"},

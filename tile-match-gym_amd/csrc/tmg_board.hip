@@ -43,6 +43,10 @@ namespace tmg {
         __builtin_amdgcn_wave_barrier();                         \
     } while (0)
 #endif
+#ifndef TMG_XCD
+#define TMG_XCD 1          // XCD-aware workgroup -> env mapping
+#endif
+
 // compiler-only ordering point between a wave's LDS loads and later stores
 #define WFENCE() __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront")
 
@@ -101,6 +105,20 @@ __device__ uint64_t g_stamps[kStampEnvs * kStampSlots];
 #define STAMP(e, slot) ((void)0)
 #define STAMPV(e, slot, v) ((void)0)
 #endif
+
+// Workgroup -> first env.  The dispatcher hands workgroup b to XCD b % 8; with
+// TMG_XCD the host pads the grid to a multiple of 8 and XCD x gets the
+// contiguous env block [x*G/8, (x+1)*G/8), so the per-env arrays (actions,
+// timer, outputs, masks) are touched by one XCD's L2 per cache line instead
+// of eight (speed only: correctness never depends on the placement).
+__device__ __forceinline__ int64_t wg_env0() {
+#if TMG_XCD
+    const int64_t per = gridDim.x >> 3;
+    return ((int64_t)(blockIdx.x & 7) * per + (blockIdx.x >> 3)) * TMG_WPB;
+#else
+    return (int64_t)blockIdx.x * TMG_WPB;
+#endif
+}
 
 // scalar slots in LDS (lane-0 sections publish through these)
 enum : int { SC_NACT = 0, SC_NNEW, SC_ERR, SC_NZ, SC_A, SC_B, SC_C, SC_D, SC_COUNT = 16 };
@@ -1271,7 +1289,7 @@ __global__ TMG_LAUNCH_BOUNDS void step_kernel(
     const int lane = threadIdx.x & 63;
     const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
     WS &w = reinterpret_cast<WS *>(smem)[wv];
-    const int64_t e = (int64_t)blockIdx.x * TMG_WPB + wv;
+    const int64_t e = wg_env0() + wv;
     if (e >= n) return;
 
     const int N = P.N, W = P.W;
@@ -1369,7 +1387,7 @@ __global__ TMG_LAUNCH_BOUNDS void reset_kernel(Params P, int64_t n, int8_t *__re
     const int lane = threadIdx.x & 63;
     const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
     WS &w = reinterpret_cast<WS *>(smem)[wv];
-    const int64_t e = (int64_t)blockIdx.x * TMG_WPB + wv;
+    const int64_t e = wg_env0() + wv;
     if (e >= n) return;
     if (env_mask && !__builtin_amdgcn_readfirstlane((int)env_mask[e])) return;
     const int N = P.N, W = P.W;
@@ -1392,7 +1410,7 @@ __global__ TMG_LAUNCH_BOUNDS void effective_kernel(Params P, int64_t n, const in
     const int lane = threadIdx.x & 63;
     const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
     WS &w = reinterpret_cast<WS *>(smem)[wv];
-    const int64_t e = (int64_t)blockIdx.x * TMG_WPB + wv;
+    const int64_t e = wg_env0() + wv;
     if (e >= n) return;
     load_board(P, w, lane, board + e * 2 * P.N);
     WSYNC();

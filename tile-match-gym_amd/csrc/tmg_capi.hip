@@ -38,7 +38,9 @@ static int launch_all(int which, tmg_ctx *ctx, int64_t n, int8_t *board, uint64_
                       const int32_t *actions, int32_t *reward, int32_t *n_new, int32_t *n_act, uint8_t *flags,
                       uint64_t *eff, const uint8_t *env_mask, int trust_eff, int autoreset, hipStream_t s) {
     const dim3 block(64 * TMG_WPB);
-    const dim3 grid((unsigned)((n + TMG_WPB - 1) / TMG_WPB));
+    int64_t nwg = (n + TMG_WPB - 1) / TMG_WPB;
+    if (TMG_XCD) nwg = (nwg + 7) & ~(int64_t)7;                 // wg_env0(): 8 equal XCD blocks
+    const dim3 grid((unsigned)nwg);
     const size_t lean = sizeof(tmg::Ws<MAXN, false>) * TMG_WPB;
     const size_t gen = sizeof(tmg::Ws<MAXN, true>) * TMG_WPB;
     if (which == 0) {

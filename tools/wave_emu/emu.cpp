@@ -181,10 +181,9 @@ static void body_thunk(void *p) { (*reinterpret_cast<F *>(p))(); }
 
 template <class F>
 static void run_blocks(int64_t n, size_t lds, F kernel) {
-    // one wave per block; EMU_EPW > 1 exercises the kernels' grid-stride env loop
-    int epw = 1;
-    if (const char *v = getenv("EMU_EPW")) epw = atoi(v) > 0 ? atoi(v) : 1;
-    const int64_t nblocks = (n + epw - 1) / epw;
+    // one wave per block; the grid is padded to 8 XCD blocks like the host launcher does
+    int64_t nblocks = n;
+    if (TMG_XCD) nblocks = (nblocks + 7) & ~(int64_t)7;
     emu_grid_dim.x = (unsigned)nblocks;
     for (int64_t b = 0; b < nblocks; b++) {
         std::vector<unsigned char> smem(lds);          // exactly sized: ASan catches any overrun
