@@ -65,7 +65,27 @@ struct Params {
     uint32_t thr;                 // Lemire threshold (2^32 - k) % k; 0 for powers of two
     uint32_t cmag, cm1mag;        // ceil(2^20 / C), ceil(2^20 / (C-1)): exact x / C for x < 2^10
     const uint64_t *jump;         // [64][4] jump-ahead table
+    // scalar-bitboard geometry (tmg_sb.hip; boards of <= 128 cells): cell p is
+    // bit p>>1 of word p&1.  [0] even cells, [1] odd cells.
+    uint64_t sb_nl[2];            // column <= C-2 (a right neighbour exists)
+    uint64_t sb_nf[2];            // column >= 1
+    uint64_t sb_h[2];             // column <= C-3 (a horizontal line may start)
+    uint64_t sb_z;                // one column's cells of one word, from bit 0
+    uint64_t sb_in[2], sb_u[2], sb_v[2];   // cells of the board / of rows >= 1 / of rows >= 2
+    const uint64_t *sb_rows;      // [R][4]: row r's cells (a, b), rows 0..r's cells (a, b)
 };
+
+// host: the per-row masks of Params::sb_rows (boards of <= 128 cells)
+inline void build_sb_rows(int R, int C, uint64_t *tab) {
+    for (int r = 0; r < R; r++) {
+        uint64_t m[4] = {0, 0, 0, 0};
+        for (int p = 0; p < (r + 1) * C && p < 128; p++) {
+            if (p >= r * C) m[p & 1] |= 1ULL << (p >> 1);
+            m[2 + (p & 1)] |= 1ULL << (p >> 1);
+        }
+        for (int i = 0; i < 4; i++) tab[r * 4 + i] = m[i];
+    }
+}
 
 inline Params make_params(int R, int C, int k, int smask, int num_moves, const uint64_t *jump) {
     Params P;
@@ -78,6 +98,24 @@ inline Params make_params(int R, int C, int k, int smask, int num_moves, const u
     P.cmag = ((1u << 20) + (uint32_t)C - 1) / (uint32_t)C;
     P.cm1mag = C > 1 ? ((1u << 20) + (uint32_t)C - 2) / (uint32_t)(C - 1) : 0u;
     P.jump = jump;
+    for (int w = 0; w < 2; w++) P.sb_nl[w] = P.sb_nf[w] = P.sb_h[w] = P.sb_in[w] = P.sb_u[w] = P.sb_v[w] = 0;
+    P.sb_z = 0;
+    P.sb_rows = nullptr;
+    if (P.N <= 128) {
+        for (int p = 0; p < P.N; p++) {
+            const int c = p % C, w = p & 1, b = p >> 1;
+            P.sb_in[w] |= 1ULL << b;
+            if (p >= C) P.sb_u[w] |= 1ULL << b;
+            if (p >= 2 * C) P.sb_v[w] |= 1ULL << b;
+            if (c <= C - 2) P.sb_nl[w] |= 1ULL << b;
+            if (c >= 1) P.sb_nf[w] |= 1ULL << b;
+            if (c <= C - 3) P.sb_h[w] |= 1ULL << b;
+        }
+        // even C: a column sits in one word with stride C/2; odd C: it alternates
+        // words, stride C within each
+        const int stride = (C & 1) ? C : C / 2;
+        for (int b = 0; b < 64; b += stride) P.sb_z |= 1ULL << b;
+    }
     return P;
 }
 
@@ -1256,6 +1294,8 @@ __device__ __forceinline__ int board_move(const Params &P, Ws<MAXN, GEN> &w, int
     return elim;
 }
 
+#include "tmg_sb.hip"
+
 // ------------------------------------------------------------------ kernels
 __device__ __forceinline__ LaneJump load_jump(const Params &P, int lane, const Rng &g) {
     const uint64_t *t = P.jump + lane * 4;
@@ -1278,7 +1318,9 @@ __device__ __forceinline__ void store_rng(uint64_t *p, const Rng &g, int lane) {
 // TileMatchEnv.step for one env per wave (tile_match_env.py:93-112).
 // GEN=false: lean variant for boards that can hold no special (no specials
 // enabled, cached effective mask trusted).
-template <int MAXN, bool GEN>
+// SBNB > 0 (lean variant, <= 128 cells): the scalar-bitboard path of
+// tmg_sb.hip with SBNB colour planes; CODD = C is odd.
+template <int MAXN, bool GEN, int SBNB = 0, bool CODD = false>
 __global__ TMG_LAUNCH_BOUNDS void step_kernel(
     Params P, int64_t n, int8_t *__restrict__ board, uint64_t *__restrict__ rng, int32_t *__restrict__ timer,
     const int32_t *__restrict__ actions, int32_t *__restrict__ reward, int32_t *__restrict__ n_new,
@@ -1341,13 +1383,15 @@ __global__ TMG_LAUNCH_BOUNDS void step_kernel(
     bool changed = false;
     STAMP(e, 1);
     if (effective) {
-        elim = board_move(P, w, lane, J, g, cl, p1, p2, flags, nn, na, e);
+        if constexpr (SBNB > 0) elim = sb_move<SBNB, CODD>(P, w, lane, J, g, cl, p1, p2, flags);
+        else elim = board_move(P, w, lane, J, g, cl, p1, p2, flags, nn, na, e);
         changed = true;
     }
     STAMP(e, 4);
     int tnew = t1;
     if (done && autoreset) {                                                // reset() without a seed
-        generate_board(P, w, lane, J, g, cl);
+        if constexpr (SBNB > 0) sb_generate<SBNB, CODD>(P, w, lane, J, g, cl);
+        else generate_board(P, w, lane, J, g, cl);
         tnew = 0;
         flags |= FL_RESET;
         changed = true;
@@ -1377,7 +1421,7 @@ __global__ TMG_LAUNCH_BOUNDS void step_kernel(
 }
 
 // TileMatchEnv.reset without a seed (tile_match_env.py:84-91)
-template <int MAXN>
+template <int MAXN, int SBNB = 0, bool CODD = false>
 __global__ TMG_LAUNCH_BOUNDS void reset_kernel(Params P, int64_t n, int8_t *__restrict__ board,
                                                              uint64_t *__restrict__ rng, int32_t *__restrict__ timer,
                                                              uint64_t *__restrict__ eff,
@@ -1394,7 +1438,8 @@ __global__ TMG_LAUNCH_BOUNDS void reset_kernel(Params P, int64_t n, int8_t *__re
     Rng g = load_rng(rng + e * 5);
     const LaneJump J = load_jump(P, lane, g);
     const Cells<MAXN / 64> cl = make_cells<MAXN / 64>(P, lane);
-    generate_board(P, w, lane, J, g, cl);                                   // board.py:95-109
+    if constexpr (SBNB > 0) sb_generate<SBNB, CODD>(P, w, lane, J, g, cl);   // board.py:95-109
+    else generate_board(P, w, lane, J, g, cl);
     store_board(P, w, lane, board + e * 2 * N);
     store_rng(rng + e * 5, g, lane);
     for (int i = lane; i < W; i += 64) eff[e * W + i] = w.effw[i];

@@ -2,6 +2,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 
@@ -28,10 +29,41 @@ struct tmg_ctx {
     int device;
     tmg::Params P;
     uint64_t *d_jump;
+    uint64_t *d_sbrows;
     int maxn;
+    int sb;        // scalar-bitboard kernels usable (<= 128 cells, C <= 63); TMG_SB=0 disables (A/B)
 };
 
 using tmg::Params;
+
+static size_t lean_lds(const tmg_ctx *) { return sizeof(tmg::Ws<128, false>) * TMG_WPB; }
+
+// lean step / reset on scalar bitboards (tmg_sb.hip), NB colour planes, CODD = C odd
+template <int NB, bool CODD>
+static void launch_sb(int which, tmg_ctx *ctx, dim3 grid, dim3 block, size_t lds, int64_t n, int8_t *board,
+                      uint64_t *rng, int32_t *timer, const int32_t *actions, int32_t *reward, int32_t *n_new,
+                      int32_t *n_act, uint8_t *flags, uint64_t *eff, const uint8_t *env_mask, int trust_eff,
+                      int autoreset, hipStream_t s) {
+    if (which == 0)
+        hipLaunchKernelGGL((tmg::step_kernel<128, false, NB, CODD>), grid, block, lds, s, ctx->P, n, board, rng, timer,
+                           actions, reward, n_new, n_act, flags, eff, trust_eff, autoreset);
+    else
+        hipLaunchKernelGGL((tmg::reset_kernel<128, NB, CODD>), grid, block, lds, s, ctx->P, n, board, rng, timer, eff,
+                           env_mask);
+}
+
+template <bool CODD>
+static void launch_sb_nb(int which, tmg_ctx *ctx, dim3 grid, dim3 block, size_t lds, int64_t n, int8_t *board,
+                         uint64_t *rng, int32_t *timer, const int32_t *actions, int32_t *reward, int32_t *n_new,
+                         int32_t *n_act, uint8_t *flags, uint64_t *eff, const uint8_t *env_mask, int trust_eff,
+                         int autoreset, hipStream_t s) {
+    switch (tmg::sb_planes(ctx->P.k)) {
+    case 1: launch_sb<1, CODD>(which, ctx, grid, block, lds, n, board, rng, timer, actions, reward, n_new, n_act, flags, eff, env_mask, trust_eff, autoreset, s); break;
+    case 2: launch_sb<2, CODD>(which, ctx, grid, block, lds, n, board, rng, timer, actions, reward, n_new, n_act, flags, eff, env_mask, trust_eff, autoreset, s); break;
+    case 3: launch_sb<3, CODD>(which, ctx, grid, block, lds, n, board, rng, timer, actions, reward, n_new, n_act, flags, eff, env_mask, trust_eff, autoreset, s); break;
+    default: launch_sb<4, CODD>(which, ctx, grid, block, lds, n, board, rng, timer, actions, reward, n_new, n_act, flags, eff, env_mask, trust_eff, autoreset, s); break;
+    }
+}
 
 template <int MAXN>
 static int launch_all(int which, tmg_ctx *ctx, int64_t n, int8_t *board, uint64_t *rng, int32_t *timer,
@@ -43,6 +75,18 @@ static int launch_all(int which, tmg_ctx *ctx, int64_t n, int8_t *board, uint64_
     const dim3 grid((unsigned)nwg);
     const size_t lean = sizeof(tmg::Ws<MAXN, false>) * TMG_WPB;
     const size_t gen = sizeof(tmg::Ws<MAXN, true>) * TMG_WPB;
+    if constexpr (MAXN == 128) {
+        const bool lean = which == 0 && ctx->P.smask == 0 && trust_eff;
+        if (ctx->sb && (lean || which == 1)) {
+            if (ctx->P.C & 1)
+                launch_sb_nb<true>(which, ctx, grid, block, lean_lds(ctx), n, board, rng, timer, actions, reward, n_new,
+                                   n_act, flags, eff, env_mask, trust_eff, autoreset, s);
+            else
+                launch_sb_nb<false>(which, ctx, grid, block, lean_lds(ctx), n, board, rng, timer, actions, reward, n_new,
+                                    n_act, flags, eff, env_mask, trust_eff, autoreset, s);
+            return hip_check(hipGetLastError(), "kernel launch");
+        }
+    }
     if (which == 0) {
         // lean variant: no special can exist (none enabled) and the cached mask is trusted
         if (ctx->P.smask == 0 && trust_eff)
@@ -99,6 +143,8 @@ int tmg_create(tmg_ctx **out, int device, int rows, int cols, int colours, uint3
     c->P = tmg::make_params(rows, cols, colours, (int)specials_mask, num_moves, nullptr);
     Params &P = c->P;
     c->maxn = P.N <= 128 ? 128 : 512;
+    const char *sbenv = getenv("TMG_SB");
+    c->sb = P.N <= 128 && P.C <= 63 && !(sbenv && sbenv[0] == '0');
     uint64_t tab[64 * 4];
     tmg::build_jump_table(tab);
     rc = hip_check(hipMalloc(&c->d_jump, sizeof tab), "hipMalloc");
@@ -106,6 +152,15 @@ int tmg_create(tmg_ctx **out, int device, int rows, int cols, int colours, uint3
     rc = hip_check(hipMemcpy(c->d_jump, tab, sizeof tab, hipMemcpyHostToDevice), "hipMemcpy");
     if (rc) { (void)hipFree(c->d_jump); delete c; return rc; }
     P.jump = c->d_jump;
+    c->d_sbrows = nullptr;
+    if (P.N <= 128) {
+        uint64_t rows[64 * 4];
+        tmg::build_sb_rows(P.R, P.C, rows);
+        rc = hip_check(hipMalloc(&c->d_sbrows, sizeof rows), "hipMalloc");
+        if (!rc) rc = hip_check(hipMemcpy(c->d_sbrows, rows, sizeof rows, hipMemcpyHostToDevice), "hipMemcpy");
+        if (rc) { (void)hipFree(c->d_jump); if (c->d_sbrows) (void)hipFree(c->d_sbrows); delete c; return rc; }
+        P.sb_rows = c->d_sbrows;
+    }
     *out = c;
     return 0;
 }
@@ -113,6 +168,7 @@ int tmg_create(tmg_ctx **out, int device, int rows, int cols, int colours, uint3
 int tmg_destroy(tmg_ctx *ctx) {
     if (!ctx) return 0;
     (void)hipFree(ctx->d_jump);
+    if (ctx->d_sbrows) (void)hipFree(ctx->d_sbrows);
     delete ctx;
     return 0;
 }

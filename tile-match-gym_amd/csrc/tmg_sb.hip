@@ -1,0 +1,383 @@
+// tmg_sb.hip — scalar bitboards: the no-specials path for boards of <= 128
+// cells (c2/c4: 10x10, 4 colours).  Included by tmg_board.hip.
+//
+// Cell p = r*C + c is bit p>>1 of word p&1 (`a` = even cells, `b` = odd
+// cells), and a colour is NB bit-planes of (colour - 1).  With one wave per
+// board, lane j's PCG output j carries the colours of cells 2j and 2j+1, so
+// one __ballot per plane turns a lane-parallel draw straight into bitboards.
+// Everything wave-uniform — line detection (get_colour_lines' first pass,
+// board.py:158-193), its perpendicular pass (:195-214), the clear mask of a
+// cascade step and remove_colour_lines' first line (:120-131) — then runs as
+// 64-bit SALU ops on SGPRs, leaving the VALU to the RNG and the lane-parallel
+// gravity/refill scatter.  The int8 LDS board stays in sync at the points the
+// shared code reads it (effective-action scan, shuffle, store).
+
+struct Pair {
+    uint64_t a, b;
+};
+__device__ __forceinline__ Pair operator&(Pair x, Pair y) { return Pair{x.a & y.a, x.b & y.b}; }
+__device__ __forceinline__ Pair operator|(Pair x, Pair y) { return Pair{x.a | y.a, x.b | y.b}; }
+__device__ __forceinline__ Pair operator^(Pair x, Pair y) { return Pair{x.a ^ y.a, x.b ^ y.b}; }
+__device__ __forceinline__ Pair andn(Pair x, Pair y) { return Pair{x.a & ~y.a, x.b & ~y.b}; }   // x & ~y
+__device__ __forceinline__ bool nonzero(Pair x) { return (x.a | x.b) != 0ULL; }
+__device__ __forceinline__ int popc(Pair x) { return __popcll(x.a) + __popcll(x.b); }
+__device__ __forceinline__ uint64_t lowmask(int n) { return n >= 64 ? ~0ULL : ((1ULL << n) - 1ULL); }   // n >= 0
+__device__ __forceinline__ bool test(Pair x, int p) { return (((p & 1) ? x.b : x.a) >> (p >> 1)) & 1ULL; }
+__device__ __forceinline__ int ctz64(uint64_t x) { return __ffsll((unsigned long long)x) - 1; }
+
+// per-row masks from Params::sb_rows, read through the scalar cache
+#ifndef TMG_CONST_AS
+#define TMG_CONST_AS __attribute__((address_space(4)))
+#endif
+typedef const TMG_CONST_AS uint64_t sbrow_t;
+__device__ __forceinline__ Pair sb_row(const Params &P, int r) {           // cells of row r
+    const sbrow_t *t = (const sbrow_t *)P.sb_rows + 4 * r;
+    return Pair{t[0], t[1]};
+}
+__device__ __forceinline__ Pair sb_rows_to(const Params &P, int r) {       // cells of rows 0..r
+    const sbrow_t *t = (const sbrow_t *)P.sb_rows + 4 * r;
+    return Pair{t[2], t[3]};
+}
+
+// fwd: result[q] = x[q - d] (content moves d cells forward); bwd: result[q] =
+// x[q + d].  ODD = parity of d.  Requires d <= 127 - 1 (shifts < 64).
+template <bool ODD>
+__device__ __forceinline__ Pair fwd(Pair x, int d) {
+    if constexpr (ODD) return Pair{x.b << ((d + 1) >> 1), x.a << ((d - 1) >> 1)};
+    else return Pair{x.a << (d >> 1), x.b << (d >> 1)};
+}
+template <bool ODD>
+__device__ __forceinline__ Pair bwd(Pair x, int d) {
+    if constexpr (ODD) return Pair{x.b >> ((d - 1) >> 1), x.a >> ((d + 1) >> 1)};
+    else return Pair{x.a >> (d >> 1), x.b >> (d >> 1)};
+}
+
+template <int NB>
+struct SB {
+    Pair p[NB];
+};
+
+// number of bit-planes for colour codes 0..k-1
+__host__ __device__ constexpr int sb_planes(int k) { return k <= 2 ? 1 : k <= 4 ? 2 : k <= 8 ? 3 : 4; }
+
+// bitboards from the LDS colour plane (cells 2*lane, 2*lane+1)
+template <int NB>
+__device__ __forceinline__ SB<NB> sb_from_lds(const Params &P, const int8_t *brd, int lane) {
+    const int q0 = 2 * lane, N = P.N;
+    const int x0 = q0 < N ? (int)brd[q0] - 1 : 0;
+    const int x1 = q0 + 1 < N ? (int)brd[q0 + 1] - 1 : 0;
+    SB<NB> s;
+#pragma unroll
+    for (int b = 0; b < NB; b++) {
+        s.p[b].a = __ballot((x0 >> b) & 1);
+        s.p[b].b = __ballot((x1 >> b) & 1);
+    }
+    return s;
+}
+
+template <int NB>
+__device__ __forceinline__ void sb_to_lds(const Params &P, int8_t *brd, int8_t *trash, int lane, const SB<NB> &s) {
+    const int q0 = 2 * lane, N = P.N;
+    int x0 = 1, x1 = 1;
+#pragma unroll
+    for (int b = 0; b < NB; b++) {
+        x0 += (int)((s.p[b].a >> lane) & 1ULL) << b;
+        x1 += (int)((s.p[b].b >> lane) & 1ULL) << b;
+    }
+    *(q0 < N ? brd + q0 : trash + lane) = (int8_t)x0;
+    *(q0 + 1 < N ? brd + q0 + 1 : trash + 64 + lane) = (int8_t)x1;
+}
+
+// get_colour_lines' first pass on a full board (board.py:158-193): va = a
+// vertical line has its bottom cell here (r >= 2, same colour as the two cells
+// above), ha = a horizontal run of >= 3 may start here (c <= C-3).  neU / neR:
+// colour differs from the cell above / to the right (garbage at the edges).
+struct SBDet {
+    Pair va, ha, neU, neR;
+};
+
+template <int NB, bool CODD>
+__device__ __forceinline__ SBDet sb_detect(const Params &P, const SB<NB> &s) {
+    const int C = P.C;
+    SBDet d;
+    d.neU = Pair{0, 0};
+    d.neR = Pair{0, 0};
+#pragma unroll
+    for (int b = 0; b < NB; b++) {
+        d.neU = d.neU | (s.p[b] ^ fwd<CODD>(s.p[b], C));
+        d.neR = d.neR | (s.p[b] ^ bwd<true>(s.p[b], 1));
+    }
+    d.va = andn(Pair{P.sb_v[0], P.sb_v[1]}, d.neU | fwd<CODD>(d.neU, C));
+    d.ha = andn(Pair{P.sb_h[0], P.sb_h[1]}, d.neR | bwd<true>(d.neR, 1));
+    return d;
+}
+
+// bottom-most row holding a line start (get_colour_lines scans rows bottom-up
+// and stops at the first row with a line), or -1
+__device__ __forceinline__ int sb_bottom_row(const Params &P, const SBDet &d) {
+    const Pair m = d.va | d.ha;
+    const int pa = m.a ? 2 * (63 - __clzll(m.a)) : -1;
+    const int pb = m.b ? 2 * (63 - __clzll(m.b)) + 1 : -1;
+    const int pm = pa > pb ? pa : pb;
+    return pm < 0 ? -1 : div_c(P, pm);
+}
+
+// remove_colour_lines (board.py:120-131): row of the first coord of the first
+// line get_colour_lines returns, or -1.  In the bottom row, columns run left
+// to right with the vertical check first; a vertical line starts at the top
+// of its run (:166-172).
+template <int NB, bool CODD>
+__device__ __forceinline__ int sb_first_line_row(const Params &P, const SB<NB> &s) {
+    const SBDet d = sb_detect<NB, CODD>(P, s);
+    const int rs = sb_bottom_row(P, d);
+    if (rs < 0) return -1;
+    const int C = P.C;
+    const Pair m = (d.va | d.ha) & sb_row(P, rs);
+    const int ca = m.a ? 2 * ctz64(m.a) : 1 << 20;
+    const int cb = m.b ? 2 * ctz64(m.b) + 1 : 1 << 20;
+    const int c0 = ca < cb ? ca : cb;
+    if (!test(d.va, c0)) return rs;
+    int t = c0 - 2 * C;
+    while (t >= C && !test(d.neU, t)) t -= C;
+    return div_c(P, t);
+}
+
+// One cascade step when no special can exist (board.py:367-376 with every
+// line a normal match): the union of get_colour_lines' lines in row rs —
+// first-pass lines (coords K) plus the perpendicular pass, which from every
+// coord walks each axis over non-coord cells of the same colour and keeps
+// runs of >= 3 (:195-214).
+template <int NB, bool CODD>
+__device__ __forceinline__ Pair sb_clear(const Params &P, const SBDet &d, int rs) {
+    const int C = P.C;
+    const Pair inb{P.sb_in[0], P.sb_in[1]};
+    const Pair row = sb_row(P, rs);
+    const Pair nf{P.sb_nf[0], P.sb_nf[1]};
+    const Pair eqR = andn(Pair{P.sb_nl[0], P.sb_nl[1]}, d.neR);   // same colour as the right neighbour
+    const Pair eqU = andn(Pair{P.sb_u[0], P.sb_u[1]}, d.neU);      // same colour as the cell above
+    // first-pass coords: horizontal runs of row rs, vertical runs ending in it
+    const Pair h = d.ha & row;
+    Pair K = h | fwd<true>(h, 1) | fwd<false>(h, 2);
+    const Pair v = d.va & row;
+    if (nonzero(v)) {
+        Pair t = bwd<false>(v, 2 * C);
+        K = K | v | bwd<CODD>(v, C) | t;
+        for (;;) {
+            t = bwd<CODD>(t & eqU, C);
+            if (!nonzero(t)) break;
+            K = K | t;
+        }
+    }
+    Pair clr = K;
+    const Pair walk = andn(inb, K);
+    // horizontal runs through coords
+    const Pair r1 = fwd<true>(K & eqR, 1) & walk;
+    const Pair l1 = bwd<true>(K & nf, 1) & eqR & walk;
+    if (nonzero(r1 | l1)) {
+        const Pair r2 = fwd<true>(r1 & eqR, 1) & walk;
+        const Pair l2 = bwd<true>(l1 & nf, 1) & eqR & walk;
+        const Pair q = K & (bwd<false>(r2, 2) | fwd<false>(l2, 2) | (bwd<true>(r1, 1) & fwd<true>(l1, 1)));
+        if (nonzero(q)) {
+            Pair f = fwd<true>(q & eqR, 1) & walk;
+            while (nonzero(f)) { clr = clr | f; f = fwd<true>(f & eqR, 1) & walk; }
+            Pair g = bwd<true>(q & nf, 1) & eqR & walk;
+            while (nonzero(g)) { clr = clr | g; g = bwd<true>(g & nf, 1) & eqR & walk; }
+        }
+    }
+    // vertical runs through coords
+    const Pair d1 = fwd<CODD>(K, C) & eqU & walk;
+    const Pair u1 = bwd<CODD>(K & eqU, C) & walk;
+    if (nonzero(d1 | u1)) {
+        const Pair d2 = fwd<CODD>(d1, C) & eqU & walk;
+        const Pair u2 = bwd<CODD>(u1 & eqU, C) & walk;
+        const Pair q = K & (fwd<false>(u2, 2 * C) | bwd<false>(d2, 2 * C) | (fwd<CODD>(u1, C) & bwd<CODD>(d1, C)));
+        if (nonzero(q)) {
+            Pair f = fwd<CODD>(q, C) & eqU & walk;
+            while (nonzero(f)) { clr = clr | f; f = fwd<CODD>(f, C) & eqU & walk; }
+            Pair g = bwd<CODD>(q & eqU, C) & walk;
+            while (nonzero(g)) { clr = clr | g; g = bwd<CODD>(g & eqU, C) & walk; }
+        }
+    }
+    return clr;
+}
+
+// gravity + refill (board.py:217-241) of the cleared cells E (total of them),
+// as one LDS scatter: each lane owns cells 2*lane and 2*lane+1; a kept cell
+// drops by the empties below it in its column, the top `empties` cells of a
+// column take the refill draws in row-major order.
+template <bool CODD, class WS>
+__device__ __forceinline__ void sb_gravity_refill(const Params &P, WS &w, int lane, const LaneJump &J, Rng &g,
+                                                  const Pair E, int total) {
+    const int N = P.N, C = P.C;
+    int8_t *col = w.brd;
+    const int q0 = 2 * lane, q1 = q0 + 1;
+    const int r0 = div_c(P, q0), c0 = q0 - r0 * C;
+    const int r1 = div_c(P, q1), c1 = q1 - r1 * C;
+    // the cells of a column: zcol shifted to the column's first bit in each word
+    uint64_t ca0, cb0, ca1, cb1;
+    if constexpr (CODD) {
+        // rows with (r + c) even are even cells
+        const int sa0 = ((c0 & 1) * C + c0) >> 1, sb0 = ((1 - (c0 & 1)) * C + c0) >> 1;
+        const int sa1 = ((c1 & 1) * C + c1) >> 1, sb1 = ((1 - (c1 & 1)) * C + c1) >> 1;
+        ca0 = P.sb_z << sa0; cb0 = P.sb_z << sb0;
+        ca1 = P.sb_z << sa1; cb1 = P.sb_z << sb1;
+    } else {
+        // cell 2*lane has an even column (all even cells), 2*lane+1 an odd one
+        ca0 = P.sb_z << (c0 >> 1); cb0 = 0;
+        ca1 = 0; cb1 = P.sb_z << (c1 >> 1);
+    }
+    const uint64_t ea0 = E.a & ca0, eb0 = E.b & cb0, ea1 = E.a & ca1, eb1 = E.b & cb1;
+    const int ec0 = __popcll(ea0) + __popcll(eb0);
+    const int ec1 = __popcll(ea1) + __popcll(eb1);
+    // empties strictly below: cells > q of the column
+    const int below0 = __popcll(ea0 & ~lowmask((q0 >> 1) + 1)) + __popcll(eb0 & ~lowmask((q0 + 1) >> 1));
+    const int below1 = __popcll(ea1 & ~lowmask((q1 >> 1) + 1)) + __popcll(eb1 & ~lowmask((q1 + 1) >> 1));
+    const bool v0 = q0 < N, v1 = q1 < N;
+    const bool e0 = v0 && ((E.a >> lane) & 1ULL), e1 = v1 && ((E.b >> lane) & 1ULL);
+    const bool n0 = v0 && r0 < ec0, n1 = v1 && r1 < ec1;   // refilled after gravity
+    const uint64_t NA = __ballot(n0), NBm = __ballot(n1);
+    const uint64_t lt = lanemask_lt(lane);
+    const int rank0 = __popcll(NA & lt) + __popcll(NBm & lt);
+    const int rank1 = rank0 + (n0 ? 1 : 0);
+    const int8_t x0 = col[v0 ? q0 : 0], x1 = col[v1 ? q1 : 0];
+    draw_colours(P, lane, J, g, total, w.u.draw, w.trash);
+    WSYNC();
+    const int8_t d0 = (int8_t)w.u.draw[n0 ? rank0 : 0], d1 = (int8_t)w.u.draw[n1 ? rank1 : 0];
+    WFENCE();
+    *(v0 && !e0 ? col + q0 + below0 * C : w.trash + lane) = x0;
+    *(v1 && !e1 ? col + q1 + below1 * C : w.trash + 64 + lane) = x1;
+    *(n0 ? col + q0 : w.trash + 128 + lane) = d0;
+    *(n1 ? col + q1 : w.trash + 192 + lane) = d1;
+    WSYNC();
+}
+
+// rows 0..row (M = (row+1)*C cells) <- Generator.integers(1, k+1, M)
+// (board.py:97 generate, :129 remove_colour_lines), merged into the
+// bitboards.  Lane j evaluates PCG output j by jump-ahead (as draw_colours);
+// M <= 128 is one 64-output pass.
+template <int NB, class WS>
+__device__ __forceinline__ void sb_draw_rows(const Params &P, WS &w, int lane, const LaneJump &J, Rng &g, int row,
+                                             SB<NB> &s) {
+    const uint32_t k = (uint32_t)P.k;
+    const int M = (row + 1) * P.C;
+    const Pair m = sb_rows_to(P, row);
+    if (k == 1) {                                        // rng == 0: numpy draws nothing, every colour is 1
+#pragma unroll
+        for (int b = 0; b < NB; b++) s.p[b] = andn(s.p[b], m);
+        return;
+    }
+    const int off = (int)(g.h >> 32) & 1;                // draw 0 is the buffered half-word
+    const uint32_t cbuf = (uint32_t)(((uint64_t)(uint32_t)g.h * k) >> 32);
+    const bool rbuf = off && (uint32_t)((uint64_t)(uint32_t)g.h * k) < P.thr;
+    const int need = M - off;
+    const int n64 = (need + 1) >> 1;
+    const U128 sj = add128(mul128(J.Aj, U128{g.slo, g.shi}), J.incG);
+    const uint64_t out = xsl_rr(sj);
+    const uint64_t m0 = (uint64_t)(uint32_t)out * k, m1 = (out >> 32) * k;
+    const bool ok0 = lane < n64, ok1 = 2 * lane + 1 < need;
+    const bool rej = (ok0 && (uint32_t)m0 < P.thr) || (ok1 && (uint32_t)m1 < P.thr);
+    if (P.thr != 0u && (rbuf || __ballot(rej) != 0ULL)) {
+        // Lemire rejection somewhere: exact serial replay, then cell-aligned ballots
+        draw_colours(P, lane, J, g, M, w.u.draw, w.trash);
+        WSYNC();
+        const int x0 = 2 * lane < M ? (int)w.u.draw[2 * lane] - 1 : 0;
+        const int x1 = 2 * lane + 1 < M ? (int)w.u.draw[2 * lane + 1] - 1 : 0;
+#pragma unroll
+        for (int b = 0; b < NB; b++) {
+            const Pair nw{__ballot((x0 >> b) & 1), __ballot((x1 >> b) & 1)};
+            s.p[b] = andn(s.p[b], m) | (nw & m);
+        }
+        WSYNC();
+        return;
+    }
+    const uint32_t lo = (uint32_t)(m0 >> 32), hi = (uint32_t)(m1 >> 32);   // colour codes 0..k-1
+#pragma unroll
+    for (int b = 0; b < NB; b++) {
+        const uint64_t L = __ballot(ok0 && ((lo >> b) & 1u)), H = __ballot(ok1 && ((hi >> b) & 1u));
+        // off = 0: cell 2j <- lo, 2j+1 <- hi;  off = 1: cell 0 <- buffer, 2j+1 <- lo, 2j+2 <- hi
+        const Pair nw = off ? Pair{(H << 1) | ((cbuf >> b) & 1u), L} : Pair{L, H};
+        s.p[b] = andn(s.p[b], m) | (nw & m);
+    }
+    if (n64 > 0) {
+        g.slo = rdlane64(sj.lo, n64 - 1);
+        g.shi = rdlane64(sj.hi, n64 - 1);
+        g.h = ((uint64_t)(need & 1) << 32) | (uint32_t)rdlane64(out >> 32, n64 - 1);
+    } else {
+        g.h = (uint32_t)g.h;                             // only the buffered half was used
+    }
+}
+
+// "while not possible_move() or lines" (board.py:102-109, 381-391) on the
+// bitboards.  The LDS board is brought in sync before the effective-action
+// scan (whose mask it leaves in w.effw) and the shuffle.  `dirty`: s is newer
+// than the LDS board; `clean`: s is known to hold no line.
+template <int NB, bool CODD, class WS>
+__device__ __forceinline__ bool sb_ensure(const Params &P, WS &w, int lane, const LaneJump &J, Rng &g,
+                                          const Cells<WS::NP> &cl, SB<NB> &s, bool dirty, bool clean) {
+    bool shuffled = false;
+    for (;;) {
+        if (!clean) {
+            for (;;) {
+                const int r0 = sb_first_line_row<NB, CODD>(P, s);
+                if (r0 < 0) break;
+                const int row = P.R - 1 < r0 + 1 ? P.R - 1 : r0 + 1;   // colour plane only, rows 0..row
+                sb_draw_rows<NB>(P, w, lane, J, g, row, s);
+                dirty = true;
+            }
+        }
+        if (dirty) {
+            WFENCE();
+            sb_to_lds<NB>(P, w.brd, w.trash, lane, s);
+            WSYNC();
+            dirty = false;
+        }
+        if (scan_effective(P, w, lane, cl, true)) break;
+        WSYNC();
+        shuffle(P, w, lane, g);
+        s = sb_from_lds<NB>(P, w.brd, lane);
+        shuffled = true;
+        clean = false;
+    }
+    WSYNC();
+    return shuffled;
+}
+
+// generate_board, board.py:95-109 (types all 1; colours from the env stream)
+template <int NB, bool CODD, class WS>
+__device__ __forceinline__ void sb_generate(const Params &P, WS &w, int lane, const LaneJump &J, Rng &g,
+                                            const Cells<WS::NP> &cl) {
+    SB<NB> s;
+#pragma unroll
+    for (int b = 0; b < NB; b++) s.p[b] = Pair{0, 0};
+    sb_draw_rows<NB>(P, w, lane, J, g, P.R - 1, s);
+    for (int p = lane; p < P.N; p += 64) w.brd[P.N + p] = 1;
+    sb_ensure<NB, CODD>(P, w, lane, J, g, cl, s, true, false);
+}
+
+// Board.move, board.py:330-395, for a board that can hold no special (every
+// type 1, no specials enabled) — the effectiveness test (:352) is the
+// caller's.  Returns eliminations; leaves the final board's effective mask in
+// w.effw.
+template <int NB, bool CODD, class WS>
+__device__ __forceinline__ int sb_move(const Params &P, WS &w, int lane, const LaneJump &J, Rng &g,
+                                       const Cells<WS::NP> &cl, int p1, int p2, int &flags) {
+    int8_t *col = w.brd;
+    if (lane == 0) {                                     // swap_coords :355 (types are all 1)
+        int8_t x = col[p1]; col[p1] = col[p2]; col[p2] = x;
+    }
+    WSYNC();
+    SB<NB> s = sb_from_lds<NB>(P, col, lane);
+    int elim = 0;
+    for (;;) {                                           // :367-376
+        const SBDet d = sb_detect<NB, CODD>(P, s);
+        const int rs = sb_bottom_row(P, d);
+        if (rs < 0) break;
+        const Pair clr = sb_clear<NB, CODD>(P, d, rs);
+        const int tot = popc(clr);
+        elim += tot;                                     // R*C - nnz(type) after the resolve (:374)
+        sb_gravity_refill<CODD>(P, w, lane, J, g, clr, tot);
+        s = sb_from_lds<NB>(P, col, lane);
+    }
+    if (sb_ensure<NB, CODD>(P, w, lane, J, g, cl, s, false, true)) flags |= FL_SHUF;   // :381-391
+    return elim;
+}

@@ -194,12 +194,51 @@ static void run_blocks(int64_t n, size_t lds, F kernel) {
     }
 }
 
+static uint64_t g_sbrows[64 * 4];
 static tmg::Params make_params(int R, int C, int k, int smask, int moves, const uint64_t *jump) {
-    return tmg::make_params(R, C, k, smask, moves, jump);
+    tmg::Params P = tmg::make_params(R, C, k, smask, moves, jump);
+    if (P.N <= 128) {
+        tmg::build_sb_rows(R, C, g_sbrows);
+        P.sb_rows = g_sbrows;
+    }
+    return P;
 }
 
 static uint64_t g_jump[256];
 static bool g_jump_init = false;
+
+static bool sb_ok(const tmg::Params &P) {
+    const char *v = getenv("TMG_SB");
+    return P.N <= 128 && P.C <= 63 && !(v && v[0] == '0');
+}
+
+// lean step (which 0) / reset (which 1) on scalar bitboards, as tmg_capi.hip's launch_sb
+template <int NB, bool CODD>
+static void run_sb(int which, const tmg::Params &P, int64_t n, int8_t *board, uint64_t *rng, int32_t *timer,
+                   const int32_t *actions, int32_t *reward, int32_t *n_new, int32_t *n_act, uint8_t *flags,
+                   uint64_t *eff, int trust_eff, int autoreset) {
+    if (which == 0)
+        run_blocks(n, sizeof(tmg::Ws<128, false>), [&] { tmg::step_kernel<128, false, NB, CODD>(P, n, board, rng, timer, actions, reward, n_new, n_act, flags, eff, trust_eff, autoreset); });
+    else
+        run_blocks(n, sizeof(tmg::Ws<128, false>), [&] { tmg::reset_kernel<128, NB, CODD>(P, n, board, rng, timer, eff, nullptr); });
+}
+template <bool CODD>
+static void run_sb_nb(int which, const tmg::Params &P, int64_t n, int8_t *board, uint64_t *rng, int32_t *timer,
+                      const int32_t *actions, int32_t *reward, int32_t *n_new, int32_t *n_act, uint8_t *flags,
+                      uint64_t *eff, int trust_eff, int autoreset) {
+    switch (tmg::sb_planes(P.k)) {
+    case 1: run_sb<1, CODD>(which, P, n, board, rng, timer, actions, reward, n_new, n_act, flags, eff, trust_eff, autoreset); break;
+    case 2: run_sb<2, CODD>(which, P, n, board, rng, timer, actions, reward, n_new, n_act, flags, eff, trust_eff, autoreset); break;
+    case 3: run_sb<3, CODD>(which, P, n, board, rng, timer, actions, reward, n_new, n_act, flags, eff, trust_eff, autoreset); break;
+    default: run_sb<4, CODD>(which, P, n, board, rng, timer, actions, reward, n_new, n_act, flags, eff, trust_eff, autoreset); break;
+    }
+}
+static void run_sb_any(int which, const tmg::Params &P, int64_t n, int8_t *board, uint64_t *rng, int32_t *timer,
+                       const int32_t *actions, int32_t *reward, int32_t *n_new, int32_t *n_act, uint8_t *flags,
+                       uint64_t *eff, int trust_eff, int autoreset) {
+    if (P.C & 1) run_sb_nb<true>(which, P, n, board, rng, timer, actions, reward, n_new, n_act, flags, eff, trust_eff, autoreset);
+    else run_sb_nb<false>(which, P, n, board, rng, timer, actions, reward, n_new, n_act, flags, eff, trust_eff, autoreset);
+}
 
 extern "C" {
 
@@ -209,7 +248,9 @@ int emu_step(int R, int C, int k, int smask, int moves, int64_t n, int8_t *board
     if (!g_jump_init) { tmg::build_jump_table(g_jump); g_jump_init = true; }
     tmg::Params P = make_params(R, C, k, smask, moves, g_jump);
     const bool lean = smask == 0 && trust_eff;
-    if (P.N <= 128) {
+    if (lean && sb_ok(P)) {
+        run_sb_any(0, P, n, board, rng, timer, actions, reward, n_new, n_act, flags, eff, trust_eff, autoreset);
+    } else if (P.N <= 128) {
         if (lean)
             run_blocks(n, sizeof(tmg::Ws<128, false>), [&] { tmg::step_kernel<128, false>(P, n, board, rng, timer, actions, reward, n_new, n_act, flags, eff, trust_eff, autoreset); });
         else
@@ -227,7 +268,9 @@ int emu_reset(int R, int C, int k, int smask, int moves, int64_t n, int8_t *boar
               uint64_t *eff) {
     if (!g_jump_init) { tmg::build_jump_table(g_jump); g_jump_init = true; }
     tmg::Params P = make_params(R, C, k, smask, moves, g_jump);
-    if (P.N <= 128)
+    if (sb_ok(P))
+        run_sb_any(1, P, n, board, rng, timer, nullptr, nullptr, nullptr, nullptr, nullptr, eff, 0, 0);
+    else if (P.N <= 128)
         run_blocks(n, sizeof(tmg::Ws<128, false>), [&] { tmg::reset_kernel<128>(P, n, board, rng, timer, eff, nullptr); });
     else
         run_blocks(n, sizeof(tmg::Ws<512, false>), [&] { tmg::reset_kernel<512>(P, n, board, rng, timer, eff, nullptr); });
