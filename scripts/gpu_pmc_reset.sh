@@ -3,7 +3,7 @@
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 mkdir -p gpurun_out/pmcr
 export TMPDIR=/tmp
-for sb in 1 0; do
+for sb in ${SBS:-1 0}; do
   TMG_SB=$sb timeout -k 10 60 python tools/reset_probe.py c2 || exit 1
   i=0
   for set in "SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_SMEM SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY" "SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_SCA SQ_INSTS_BRANCH SQ_WAVES GRBM_GUI_ACTIVE"; do
@@ -12,8 +12,8 @@ for sb in 1 0; do
   done
 done
 python3 - <<'PY'
-import csv, glob, collections
-for sb in (1, 0):
+import csv, glob, collections, os
+for sb in [int(x) for x in os.environ.get('SBS', '1 0').split()]:
     tot = collections.defaultdict(list)
     for f in glob.glob(f'gpurun_out/pmcr/sb{sb}_*/run_counter_collection.csv'):
         per = collections.defaultdict(lambda: collections.defaultdict(float))

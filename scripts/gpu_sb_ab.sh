@@ -10,3 +10,4 @@ for sb in 1 0; do
   tail -1 gpurun_out/bench_sb$sb.log | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print('BENCH sb=$sb', d['value'], 'ms/step', d['ms_per_step'], 'kern', d['roofline']['kernel_ms_per_launch'])"
   TMG_SB=$sb timeout -k 10 120 python tools/microbench.py --config ${CFG:-c2} || exit 1
 done
+for sb in 1 0; do TMG_SB=$sb timeout -k 10 60 python tools/reset_probe.py c2 || exit 1; done

@@ -60,32 +60,33 @@ struct SB {
 // number of bit-planes for colour codes 0..k-1
 __host__ __device__ constexpr int sb_planes(int k) { return k <= 2 ? 1 : k <= 4 ? 2 : k <= 8 ? 3 : 4; }
 
-// bitboards from the LDS colour plane (cells 2*lane, 2*lane+1)
+// The lane-side copy of the same board: colour codes (colour - 1) of cells
+// 2*lane (a) and 2*lane+1 (b), 0 outside the board.  Draws and the gravity
+// scatter update these; the bitboards are their ballots.
+struct SBC {
+    int a, b;
+};
+
 template <int NB>
-__device__ __forceinline__ SB<NB> sb_from_lds(const Params &P, const int8_t *brd, int lane) {
-    const int q0 = 2 * lane, N = P.N;
-    const int x0 = q0 < N ? (int)brd[q0] - 1 : 0;
-    const int x1 = q0 + 1 < N ? (int)brd[q0 + 1] - 1 : 0;
+__device__ __forceinline__ SB<NB> sb_planes_of(const SBC &c) {
     SB<NB> s;
 #pragma unroll
     for (int b = 0; b < NB; b++) {
-        s.p[b].a = __ballot((x0 >> b) & 1);
-        s.p[b].b = __ballot((x1 >> b) & 1);
+        s.p[b].a = __ballot((c.a >> b) & 1);
+        s.p[b].b = __ballot((c.b >> b) & 1);
     }
     return s;
 }
 
-template <int NB>
-__device__ __forceinline__ void sb_to_lds(const Params &P, int8_t *brd, int8_t *trash, int lane, const SB<NB> &s) {
+__device__ __forceinline__ SBC sb_codes_from_lds(const Params &P, const int8_t *brd, int lane) {
     const int q0 = 2 * lane, N = P.N;
-    int x0 = 1, x1 = 1;
-#pragma unroll
-    for (int b = 0; b < NB; b++) {
-        x0 += (int)((s.p[b].a >> lane) & 1ULL) << b;
-        x1 += (int)((s.p[b].b >> lane) & 1ULL) << b;
-    }
-    *(q0 < N ? brd + q0 : trash + lane) = (int8_t)x0;
-    *(q0 + 1 < N ? brd + q0 + 1 : trash + 64 + lane) = (int8_t)x1;
+    return SBC{q0 < N ? (int)brd[q0] - 1 : 0, q0 + 1 < N ? (int)brd[q0 + 1] - 1 : 0};
+}
+
+__device__ __forceinline__ void sb_codes_to_lds(const Params &P, int8_t *brd, int8_t *trash, int lane, const SBC &c) {
+    const int q0 = 2 * lane, N = P.N;
+    *(q0 < N ? brd + q0 : trash + lane) = (int8_t)(c.a + 1);
+    *(q0 + 1 < N ? brd + q0 + 1 : trash + 64 + lane) = (int8_t)(c.b + 1);
 }
 
 // get_colour_lines' first pass on a full board (board.py:158-193): va = a
@@ -123,23 +124,34 @@ __device__ __forceinline__ int sb_bottom_row(const Params &P, const SBDet &d) {
 }
 
 // remove_colour_lines (board.py:120-131): row of the first coord of the first
-// line get_colour_lines returns, or -1.  In the bottom row, columns run left
-// to right with the vertical check first; a vertical line starts at the top
-// of its run (:166-172).
+// line get_colour_lines returns, or -1.  get_colour_lines scans rows
+// bottom-up and, in the first row holding a line, columns left to right with
+// the vertical check first; so the first line is the maximum over anchor
+// cells of key = (row, -col, is_vertical), taken lane-parallel (keyA/keyB:
+// the cells' (row << 8 | 255 - col) << 1, -1 outside the board) by one DPP
+// max.  A vertical line starts at the top of its run (:166-172).
 template <int NB, bool CODD>
-__device__ __forceinline__ int sb_first_line_row(const Params &P, const SB<NB> &s) {
+__device__ __forceinline__ int sb_first_line_row(const Params &P, const SB<NB> &s, int lane, int keyA, int keyB) {
     const SBDet d = sb_detect<NB, CODD>(P, s);
-    const int rs = sb_bottom_row(P, d);
-    if (rs < 0) return -1;
+    const int vA = (int)(d.va.a >> lane) & 1, hA = (int)(d.ha.a >> lane) & 1;
+    const int vB = (int)(d.va.b >> lane) & 1, hB = (int)(d.ha.b >> lane) & 1;
+    const int ka = (vA | hA) ? keyA | vA : -1, kb = (vB | hB) ? keyB | vB : -1;
+    const int key = wave_max(ka > kb ? ka : kb);
+    if (key < 0) return -1;
+    const int rs = key >> 9;
+    if (!(key & 1)) return rs;
     const int C = P.C;
-    const Pair m = (d.va | d.ha) & sb_row(P, rs);
-    const int ca = m.a ? 2 * ctz64(m.a) : 1 << 20;
-    const int cb = m.b ? 2 * ctz64(m.b) + 1 : 1 << 20;
-    const int c0 = ca < cb ? ca : cb;
-    if (!test(d.va, c0)) return rs;
-    int t = c0 - 2 * C;
+    int t = (rs - 2) * C + 255 - ((key >> 1) & 255);
     while (t >= C && !test(d.neU, t)) t -= C;
     return div_c(P, t);
+}
+
+// the keys of sb_first_line_row for cells 2*lane, 2*lane+1
+__device__ __forceinline__ void sb_line_keys(const Params &P, int lane, int &keyA, int &keyB) {
+    const int q0 = 2 * lane, q1 = q0 + 1;
+    const int r0 = div_c(P, q0), r1 = div_c(P, q1);
+    keyA = q0 < P.N ? ((r0 << 8) | (255 - (q0 - r0 * P.C))) << 1 : -1;
+    keyB = q1 < P.N ? ((r1 << 8) | (255 - (q1 - r1 * P.C))) << 1 : -1;
 }
 
 // One cascade step when no special can exist (board.py:367-376 with every
@@ -204,10 +216,11 @@ __device__ __forceinline__ Pair sb_clear(const Params &P, const SBDet &d, int rs
 // gravity + refill (board.py:217-241) of the cleared cells E (total of them),
 // as one LDS scatter: each lane owns cells 2*lane and 2*lane+1; a kept cell
 // drops by the empties below it in its column, the top `empties` cells of a
-// column take the refill draws in row-major order.
+// column take the refill draws in row-major order.  Leaves the new board in
+// LDS and in c.
 template <bool CODD, class WS>
 __device__ __forceinline__ void sb_gravity_refill(const Params &P, WS &w, int lane, const LaneJump &J, Rng &g,
-                                                  const Pair E, int total) {
+                                                  const Pair E, int total, SBC &c) {
     const int N = P.N, C = P.C;
     int8_t *col = w.brd;
     const int q0 = 2 * lane, q1 = q0 + 1;
@@ -239,36 +252,37 @@ __device__ __forceinline__ void sb_gravity_refill(const Params &P, WS &w, int la
     const uint64_t lt = lanemask_lt(lane);
     const int rank0 = __popcll(NA & lt) + __popcll(NBm & lt);
     const int rank1 = rank0 + (n0 ? 1 : 0);
-    const int8_t x0 = col[v0 ? q0 : 0], x1 = col[v1 ? q1 : 0];
     draw_colours(P, lane, J, g, total, w.u.draw, w.trash);
     WSYNC();
     const int8_t d0 = (int8_t)w.u.draw[n0 ? rank0 : 0], d1 = (int8_t)w.u.draw[n1 ? rank1 : 0];
     WFENCE();
-    *(v0 && !e0 ? col + q0 + below0 * C : w.trash + lane) = x0;
-    *(v1 && !e1 ? col + q1 + below1 * C : w.trash + 64 + lane) = x1;
+    *(v0 && !e0 ? col + q0 + below0 * C : w.trash + lane) = (int8_t)(c.a + 1);
+    *(v1 && !e1 ? col + q1 + below1 * C : w.trash + 64 + lane) = (int8_t)(c.b + 1);
     *(n0 ? col + q0 : w.trash + 128 + lane) = d0;
     *(n1 ? col + q1 : w.trash + 192 + lane) = d1;
     WSYNC();
+    c = sb_codes_from_lds(P, col, lane);
 }
 
 // rows 0..row (M = (row+1)*C cells) <- Generator.integers(1, k+1, M)
-// (board.py:97 generate, :129 remove_colour_lines), merged into the
-// bitboards.  Lane j evaluates PCG output j by jump-ahead (as draw_colours);
-// M <= 128 is one 64-output pass.
+// (board.py:97 generate, :129 remove_colour_lines).  Lane j evaluates PCG
+// output j by jump-ahead (as draw_colours; M <= 128 is one 64-output pass)
+// and keeps the two colours of its own cells: output j holds draws 2j and
+// 2j+1, or, after a buffered half-word (draw 0), draws 2j+1 and 2j+2.
 template <int NB, class WS>
 __device__ __forceinline__ void sb_draw_rows(const Params &P, WS &w, int lane, const LaneJump &J, Rng &g, int row,
-                                             SB<NB> &s) {
+                                             SBC &c) {
     const uint32_t k = (uint32_t)P.k;
     const int M = (row + 1) * P.C;
-    const Pair m = sb_rows_to(P, row);
+    const bool inA = 2 * lane < M, inB = 2 * lane + 1 < M;
     if (k == 1) {                                        // rng == 0: numpy draws nothing, every colour is 1
-#pragma unroll
-        for (int b = 0; b < NB; b++) s.p[b] = andn(s.p[b], m);
+        c.a = inA ? 0 : c.a;
+        c.b = inB ? 0 : c.b;
         return;
     }
     const int off = (int)(g.h >> 32) & 1;                // draw 0 is the buffered half-word
-    const uint32_t cbuf = (uint32_t)(((uint64_t)(uint32_t)g.h * k) >> 32);
-    const bool rbuf = off && (uint32_t)((uint64_t)(uint32_t)g.h * k) < P.thr;
+    const uint64_t mbuf = (uint64_t)(uint32_t)g.h * k;
+    const bool rbuf = off && (uint32_t)mbuf < P.thr;
     const int need = M - off;
     const int n64 = (need + 1) >> 1;
     const U128 sj = add128(mul128(J.Aj, U128{g.slo, g.shi}), J.incG);
@@ -277,27 +291,18 @@ __device__ __forceinline__ void sb_draw_rows(const Params &P, WS &w, int lane, c
     const bool ok0 = lane < n64, ok1 = 2 * lane + 1 < need;
     const bool rej = (ok0 && (uint32_t)m0 < P.thr) || (ok1 && (uint32_t)m1 < P.thr);
     if (P.thr != 0u && (rbuf || __ballot(rej) != 0ULL)) {
-        // Lemire rejection somewhere: exact serial replay, then cell-aligned ballots
+        // Lemire rejection somewhere: exact serial replay
         draw_colours(P, lane, J, g, M, w.u.draw, w.trash);
         WSYNC();
-        const int x0 = 2 * lane < M ? (int)w.u.draw[2 * lane] - 1 : 0;
-        const int x1 = 2 * lane + 1 < M ? (int)w.u.draw[2 * lane + 1] - 1 : 0;
-#pragma unroll
-        for (int b = 0; b < NB; b++) {
-            const Pair nw{__ballot((x0 >> b) & 1), __ballot((x1 >> b) & 1)};
-            s.p[b] = andn(s.p[b], m) | (nw & m);
-        }
+        c.a = inA ? (int)w.u.draw[2 * lane] - 1 : c.a;
+        c.b = inB ? (int)w.u.draw[2 * lane + 1] - 1 : c.b;
         WSYNC();
         return;
     }
-    const uint32_t lo = (uint32_t)(m0 >> 32), hi = (uint32_t)(m1 >> 32);   // colour codes 0..k-1
-#pragma unroll
-    for (int b = 0; b < NB; b++) {
-        const uint64_t L = __ballot(ok0 && ((lo >> b) & 1u)), H = __ballot(ok1 && ((hi >> b) & 1u));
-        // off = 0: cell 2j <- lo, 2j+1 <- hi;  off = 1: cell 0 <- buffer, 2j+1 <- lo, 2j+2 <- hi
-        const Pair nw = off ? Pair{(H << 1) | ((cbuf >> b) & 1u), L} : Pair{L, H};
-        s.p[b] = andn(s.p[b], m) | (nw & m);
-    }
+    const int lo = (int)(m0 >> 32), hi = (int)(m1 >> 32);          // colour codes 0..k-1
+    const int hprev = __builtin_amdgcn_update_dpp((int)(mbuf >> 32), hi, 0x138, 0xf, 0xf, false);   // wave_shr:1
+    c.a = inA ? (off ? hprev : lo) : c.a;
+    c.b = inB ? (off ? lo : hi) : c.b;
     if (n64 > 0) {
         g.slo = rdlane64(sj.lo, n64 - 1);
         g.shi = rdlane64(sj.hi, n64 - 1);
@@ -309,32 +314,34 @@ __device__ __forceinline__ void sb_draw_rows(const Params &P, WS &w, int lane, c
 
 // "while not possible_move() or lines" (board.py:102-109, 381-391) on the
 // bitboards.  The LDS board is brought in sync before the effective-action
-// scan (whose mask it leaves in w.effw) and the shuffle.  `dirty`: s is newer
-// than the LDS board; `clean`: s is known to hold no line.
+// scan (whose mask it leaves in w.effw) and the shuffle.  `dirty`: c is newer
+// than the LDS board; `clean`: the board is known to hold no line.
 template <int NB, bool CODD, class WS>
 __device__ __forceinline__ bool sb_ensure(const Params &P, WS &w, int lane, const LaneJump &J, Rng &g,
-                                          const Cells<WS::NP> &cl, SB<NB> &s, bool dirty, bool clean) {
+                                          const Cells<WS::NP> &cl, SBC &c, bool dirty, bool clean) {
+    int keyA, keyB;
+    sb_line_keys(P, lane, keyA, keyB);
     bool shuffled = false;
     for (;;) {
         if (!clean) {
             for (;;) {
-                const int r0 = sb_first_line_row<NB, CODD>(P, s);
+                const int r0 = sb_first_line_row<NB, CODD>(P, sb_planes_of<NB>(c), lane, keyA, keyB);
                 if (r0 < 0) break;
                 const int row = P.R - 1 < r0 + 1 ? P.R - 1 : r0 + 1;   // colour plane only, rows 0..row
-                sb_draw_rows<NB>(P, w, lane, J, g, row, s);
+                sb_draw_rows<NB>(P, w, lane, J, g, row, c);
                 dirty = true;
             }
         }
         if (dirty) {
             WFENCE();
-            sb_to_lds<NB>(P, w.brd, w.trash, lane, s);
+            sb_codes_to_lds(P, w.brd, w.trash, lane, c);
             WSYNC();
             dirty = false;
         }
         if (scan_effective(P, w, lane, cl, true)) break;
         WSYNC();
         shuffle(P, w, lane, g);
-        s = sb_from_lds<NB>(P, w.brd, lane);
+        c = sb_codes_from_lds(P, w.brd, lane);
         shuffled = true;
         clean = false;
     }
@@ -346,12 +353,10 @@ __device__ __forceinline__ bool sb_ensure(const Params &P, WS &w, int lane, cons
 template <int NB, bool CODD, class WS>
 __device__ __forceinline__ void sb_generate(const Params &P, WS &w, int lane, const LaneJump &J, Rng &g,
                                             const Cells<WS::NP> &cl) {
-    SB<NB> s;
-#pragma unroll
-    for (int b = 0; b < NB; b++) s.p[b] = Pair{0, 0};
-    sb_draw_rows<NB>(P, w, lane, J, g, P.R - 1, s);
+    SBC c{0, 0};
+    sb_draw_rows<NB>(P, w, lane, J, g, P.R - 1, c);
     for (int p = lane; p < P.N; p += 64) w.brd[P.N + p] = 1;
-    sb_ensure<NB, CODD>(P, w, lane, J, g, cl, s, true, false);
+    sb_ensure<NB, CODD>(P, w, lane, J, g, cl, c, true, false);
 }
 
 // Board.move, board.py:330-395, for a board that can hold no special (every
@@ -366,18 +371,17 @@ __device__ __forceinline__ int sb_move(const Params &P, WS &w, int lane, const L
         int8_t x = col[p1]; col[p1] = col[p2]; col[p2] = x;
     }
     WSYNC();
-    SB<NB> s = sb_from_lds<NB>(P, col, lane);
+    SBC c = sb_codes_from_lds(P, col, lane);
     int elim = 0;
     for (;;) {                                           // :367-376
-        const SBDet d = sb_detect<NB, CODD>(P, s);
+        const SBDet d = sb_detect<NB, CODD>(P, sb_planes_of<NB>(c));
         const int rs = sb_bottom_row(P, d);
         if (rs < 0) break;
         const Pair clr = sb_clear<NB, CODD>(P, d, rs);
         const int tot = popc(clr);
         elim += tot;                                     // R*C - nnz(type) after the resolve (:374)
-        sb_gravity_refill<CODD>(P, w, lane, J, g, clr, tot);
-        s = sb_from_lds<NB>(P, col, lane);
+        sb_gravity_refill<CODD>(P, w, lane, J, g, clr, tot, c);
     }
-    if (sb_ensure<NB, CODD>(P, w, lane, J, g, cl, s, false, true)) flags |= FL_SHUF;   // :381-391
+    if (sb_ensure<NB, CODD>(P, w, lane, J, g, cl, c, false, true)) flags |= FL_SHUF;   // :381-391
     return elim;
 }
