@@ -1315,25 +1315,17 @@ __device__ __forceinline__ void store_rng(uint64_t *p, const Rng &g, int lane) {
     if (lane == 0) { p[0] = g.slo; p[1] = g.shi; p[2] = g.ilo; p[3] = g.ihi; p[4] = g.h; }
 }
 
-// TileMatchEnv.step for one env per wave (tile_match_env.py:93-112).
+// TileMatchEnv.step for env e on one wave (tile_match_env.py:93-112).
 // GEN=false: lean variant for boards that can hold no special (no specials
-// enabled, cached effective mask trusted).
-// SBNB > 0 (lean variant, <= 128 cells): the scalar-bitboard path of
-// tmg_sb.hip with SBNB colour planes; CODD = C is odd.
-template <int MAXN, bool GEN, int SBNB = 0, bool CODD = false>
-__global__ TMG_LAUNCH_BOUNDS void step_kernel(
-    Params P, int64_t n, int8_t *__restrict__ board, uint64_t *__restrict__ rng, int32_t *__restrict__ timer,
+// enabled, cached effective mask trusted).  SBNB > 0 (lean, <= 128 cells):
+// the scalar-bitboard path of tmg_sb.hip with SBNB colour planes; CODD = C
+// is odd.
+template <int MAXN, bool GEN, int SBNB, bool CODD>
+__device__ __forceinline__ void step_env(
+    const Params &P, Ws<MAXN, GEN> &w, int lane, int64_t e, int8_t *__restrict__ board, uint64_t *__restrict__ rng, int32_t *__restrict__ timer,
     const int32_t *__restrict__ actions, int32_t *__restrict__ reward, int32_t *__restrict__ n_new,
     int32_t *__restrict__ n_act, uint8_t *__restrict__ flags_out, uint64_t *__restrict__ eff, int trust_eff,
     int autoreset) {
-    TMG_SMEM_DECL(smem);
-    using WS = Ws<MAXN, GEN>;
-    const int lane = threadIdx.x & 63;
-    const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
-    WS &w = reinterpret_cast<WS *>(smem)[wv];
-    const int64_t e = wg_env0() + wv;
-    if (e >= n) return;
-
     const int N = P.N, W = P.W;
     STAMP(e, 0);
     const int a = __builtin_amdgcn_readfirstlane(actions[e]);             // wave-uniform loads
@@ -1383,7 +1375,7 @@ __global__ TMG_LAUNCH_BOUNDS void step_kernel(
     bool changed = false;
     STAMP(e, 1);
     if (effective) {
-        if constexpr (SBNB > 0) elim = sb_move<SBNB, CODD>(P, w, lane, J, g, cl, p1, p2, flags);
+        if constexpr (SBNB > 0) elim = sb_move<SBNB, CODD>(P, w, lane, J, g, cl, p1, p2, flags, e);
         else elim = board_move(P, w, lane, J, g, cl, p1, p2, flags, nn, na, e);
         changed = true;
     }
@@ -1418,6 +1410,24 @@ __global__ TMG_LAUNCH_BOUNDS void step_kernel(
         flags_out[e] = (uint8_t)flags;
     }
     STAMP(e, 7);
+}
+
+// TileMatchEnv.step over a batch, one wave per env.
+template <int MAXN, bool GEN, int SBNB = 0, bool CODD = false>
+__global__ TMG_LAUNCH_BOUNDS void step_kernel(
+    Params P, int64_t n, int8_t *__restrict__ board, uint64_t *__restrict__ rng, int32_t *__restrict__ timer,
+    const int32_t *__restrict__ actions, int32_t *__restrict__ reward, int32_t *__restrict__ n_new,
+    int32_t *__restrict__ n_act, uint8_t *__restrict__ flags_out, uint64_t *__restrict__ eff, int trust_eff,
+    int autoreset) {
+    TMG_SMEM_DECL(smem);
+    using WS = Ws<MAXN, GEN>;
+    const int lane = threadIdx.x & 63;
+    const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    WS &w = reinterpret_cast<WS *>(smem)[wv];
+    const int64_t e = wg_env0() + wv;
+    if (e >= n) return;
+    step_env<MAXN, GEN, SBNB, CODD>(P, w, lane, e, board, rng, timer, actions, reward, n_new, n_act, flags_out, eff,
+                                    trust_eff, autoreset);
 }
 
 // TileMatchEnv.reset without a seed (tile_match_env.py:84-91)

@@ -31,96 +31,125 @@ struct tmg_ctx {
     uint64_t *d_jump;
     uint64_t *d_sbrows;
     int maxn;
-    int sb;        // scalar-bitboard kernels usable (<= 128 cells, C <= 63); TMG_SB=0 disables (A/B)
+    int sb;          // scalar-bitboard kernels usable (<= 128 cells, C <= 63); TMG_SB=0 disables (A/B)
 };
 
 using tmg::Params;
 
-static size_t lean_lds(const tmg_ctx *) { return sizeof(tmg::Ws<128, false>) * TMG_WPB; }
+struct StepArgs {
+    int64_t n;
+    int8_t *board;
+    uint64_t *rng;
+    int32_t *timer;
+    const int32_t *actions;
+    int32_t *reward, *n_new, *n_act;
+    uint8_t *flags;
+    uint64_t *eff;
+    int trust_eff, autoreset;
+};
 
-// lean step / reset on scalar bitboards (tmg_sb.hip), NB colour planes, CODD = C odd
-template <int NB, bool CODD>
-static void launch_sb(int which, tmg_ctx *ctx, dim3 grid, dim3 block, size_t lds, int64_t n, int8_t *board,
-                      uint64_t *rng, int32_t *timer, const int32_t *actions, int32_t *reward, int32_t *n_new,
-                      int32_t *n_act, uint8_t *flags, uint64_t *eff, const uint8_t *env_mask, int trust_eff,
-                      int autoreset, hipStream_t s) {
-    if (which == 0)
-        hipLaunchKernelGGL((tmg::step_kernel<128, false, NB, CODD>), grid, block, lds, s, ctx->P, n, board, rng, timer,
-                           actions, reward, n_new, n_act, flags, eff, trust_eff, autoreset);
-    else
-        hipLaunchKernelGGL((tmg::reset_kernel<128, NB, CODD>), grid, block, lds, s, ctx->P, n, board, rng, timer, eff,
-                           env_mask);
+template <int MAXN, bool GEN, int NB, bool CODD>
+static void launch_step(dim3 grid, hipStream_t s, const Params &P, const StepArgs &a) {
+    const size_t lds = sizeof(tmg::Ws<MAXN, GEN>) * TMG_WPB;
+    hipLaunchKernelGGL((tmg::step_kernel<MAXN, GEN, NB, CODD>), grid, dim3(64 * TMG_WPB), lds, s, P, a.n, a.board,
+                       a.rng, a.timer, a.actions, a.reward, a.n_new, a.n_act, a.flags, a.eff, a.trust_eff, a.autoreset);
 }
 
+template <int MAXN, int NB, bool CODD>
+static void launch_reset(dim3 grid, hipStream_t s, const Params &P, int64_t n, int8_t *board, uint64_t *rng,
+                         int32_t *timer, uint64_t *eff, const uint8_t *env_mask) {
+    const size_t lds = sizeof(tmg::Ws<MAXN, false>) * TMG_WPB;
+    hipLaunchKernelGGL((tmg::reset_kernel<MAXN, NB, CODD>), grid, dim3(64 * TMG_WPB), lds, s, P, n, board, rng, timer,
+                       eff, env_mask);
+}
+
+// scalar-bitboard variants: NB colour planes, C odd or even
 template <bool CODD>
-static void launch_sb_nb(int which, tmg_ctx *ctx, dim3 grid, dim3 block, size_t lds, int64_t n, int8_t *board,
-                         uint64_t *rng, int32_t *timer, const int32_t *actions, int32_t *reward, int32_t *n_new,
-                         int32_t *n_act, uint8_t *flags, uint64_t *eff, const uint8_t *env_mask, int trust_eff,
-                         int autoreset, hipStream_t s) {
-    switch (tmg::sb_planes(ctx->P.k)) {
-    case 1: launch_sb<1, CODD>(which, ctx, grid, block, lds, n, board, rng, timer, actions, reward, n_new, n_act, flags, eff, env_mask, trust_eff, autoreset, s); break;
-    case 2: launch_sb<2, CODD>(which, ctx, grid, block, lds, n, board, rng, timer, actions, reward, n_new, n_act, flags, eff, env_mask, trust_eff, autoreset, s); break;
-    case 3: launch_sb<3, CODD>(which, ctx, grid, block, lds, n, board, rng, timer, actions, reward, n_new, n_act, flags, eff, env_mask, trust_eff, autoreset, s); break;
-    default: launch_sb<4, CODD>(which, ctx, grid, block, lds, n, board, rng, timer, actions, reward, n_new, n_act, flags, eff, env_mask, trust_eff, autoreset, s); break;
+static void launch_step_sb(dim3 grid, hipStream_t s, const Params &P, const StepArgs &a) {
+    switch (tmg::sb_planes(P.k)) {
+    case 1: launch_step<128, false, 1, CODD>(grid, s, P, a); break;
+    case 2: launch_step<128, false, 2, CODD>(grid, s, P, a); break;
+    case 3: launch_step<128, false, 3, CODD>(grid, s, P, a); break;
+    default: launch_step<128, false, 4, CODD>(grid, s, P, a); break;
+    }
+}
+template <bool CODD>
+static void launch_reset_sb(dim3 grid, hipStream_t s, const Params &P, int64_t n, int8_t *board, uint64_t *rng,
+                            int32_t *timer, uint64_t *eff, const uint8_t *env_mask) {
+    switch (tmg::sb_planes(P.k)) {
+    case 1: launch_reset<128, 1, CODD>(grid, s, P, n, board, rng, timer, eff, env_mask); break;
+    case 2: launch_reset<128, 2, CODD>(grid, s, P, n, board, rng, timer, eff, env_mask); break;
+    case 3: launch_reset<128, 3, CODD>(grid, s, P, n, board, rng, timer, eff, env_mask); break;
+    default: launch_reset<128, 4, CODD>(grid, s, P, n, board, rng, timer, eff, env_mask); break;
     }
 }
 
-template <int MAXN>
-static int launch_all(int which, tmg_ctx *ctx, int64_t n, int8_t *board, uint64_t *rng, int32_t *timer,
-                      const int32_t *actions, int32_t *reward, int32_t *n_new, int32_t *n_act, uint8_t *flags,
-                      uint64_t *eff, const uint8_t *env_mask, int trust_eff, int autoreset, hipStream_t s) {
-    const dim3 block(64 * TMG_WPB);
+// one wave per env: grid padded to 8 equal XCD blocks (wg_env0)
+static dim3 env_grid(int64_t n) {
     int64_t nwg = (n + TMG_WPB - 1) / TMG_WPB;
-    if (TMG_XCD) nwg = (nwg + 7) & ~(int64_t)7;                 // wg_env0(): 8 equal XCD blocks
-    const dim3 grid((unsigned)nwg);
-    const size_t lean = sizeof(tmg::Ws<MAXN, false>) * TMG_WPB;
-    const size_t gen = sizeof(tmg::Ws<MAXN, true>) * TMG_WPB;
-    if constexpr (MAXN == 128) {
-        const bool lean = which == 0 && ctx->P.smask == 0 && trust_eff;
-        if (ctx->sb && (lean || which == 1)) {
-            if (ctx->P.C & 1)
-                launch_sb_nb<true>(which, ctx, grid, block, lean_lds(ctx), n, board, rng, timer, actions, reward, n_new,
-                                   n_act, flags, eff, env_mask, trust_eff, autoreset, s);
-            else
-                launch_sb_nb<false>(which, ctx, grid, block, lean_lds(ctx), n, board, rng, timer, actions, reward, n_new,
-                                    n_act, flags, eff, env_mask, trust_eff, autoreset, s);
-            return hip_check(hipGetLastError(), "kernel launch");
+    if (TMG_XCD) nwg = (nwg + 7) & ~(int64_t)7;
+    return dim3((unsigned)nwg);
+}
+
+static int set_device(tmg_ctx *ctx) {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    if (dev != ctx->device) return hip_check(hipSetDevice(ctx->device), "hipSetDevice");
+    return 0;
+}
+
+static int do_step(tmg_ctx *ctx, const StepArgs &a, hipStream_t s) {
+    const Params &P = ctx->P;
+    const bool lean = P.smask == 0 && a.trust_eff;
+    const dim3 grid = env_grid(a.n);
+    if (ctx->maxn == 128) {
+        if (lean && ctx->sb) {
+            if (P.C & 1) launch_step_sb<true>(grid, s, P, a);
+            else launch_step_sb<false>(grid, s, P, a);
+        } else if (lean) {
+            launch_step<128, false, 0, false>(grid, s, P, a);
+        } else {
+            launch_step<128, true, 0, false>(grid, s, P, a);
         }
-    }
-    if (which == 0) {
-        // lean variant: no special can exist (none enabled) and the cached mask is trusted
-        if (ctx->P.smask == 0 && trust_eff)
-            hipLaunchKernelGGL((tmg::step_kernel<MAXN, false>), grid, block, lean, s, ctx->P, n, board, rng, timer,
-                               actions, reward, n_new, n_act, flags, eff, trust_eff, autoreset);
-        else
-            hipLaunchKernelGGL((tmg::step_kernel<MAXN, true>), grid, block, gen, s, ctx->P, n, board, rng, timer,
-                               actions, reward, n_new, n_act, flags, eff, trust_eff, autoreset);
-    } else if (which == 1) {
-        hipLaunchKernelGGL(tmg::reset_kernel<MAXN>, grid, block, lean, s, ctx->P, n, board, rng, timer, eff, env_mask);
     } else {
-        hipLaunchKernelGGL(tmg::effective_kernel<MAXN>, grid, block, lean, s, ctx->P, n, (const int8_t *)board, eff);
+        if (lean) launch_step<512, false, 0, false>(grid, s, P, a);
+        else launch_step<512, true, 0, false>(grid, s, P, a);
     }
     return hip_check(hipGetLastError(), "kernel launch");
 }
 
-static int dispatch(int which, tmg_ctx *ctx, int64_t n, int8_t *board, uint64_t *rng, int32_t *timer,
-                    const int32_t *actions, int32_t *reward, int32_t *n_new, int32_t *n_act, uint8_t *flags,
-                    uint64_t *eff, const uint8_t *env_mask, int trust_eff, int autoreset, void *stream) {
+static int do_reset(tmg_ctx *ctx, int64_t n, int8_t *board, uint64_t *rng, int32_t *timer, uint64_t *eff,
+                    const uint8_t *env_mask, hipStream_t s) {
+    const Params &P = ctx->P;
+    const dim3 grid = env_grid(n);
+    if (ctx->maxn == 128) {
+        if (ctx->sb) {
+            if (P.C & 1) launch_reset_sb<true>(grid, s, P, n, board, rng, timer, eff, env_mask);
+            else launch_reset_sb<false>(grid, s, P, n, board, rng, timer, eff, env_mask);
+        } else {
+            launch_reset<128, 0, false>(grid, s, P, n, board, rng, timer, eff, env_mask);
+        }
+    } else {
+        launch_reset<512, 0, false>(grid, s, P, n, board, rng, timer, eff, env_mask);
+    }
+    return hip_check(hipGetLastError(), "kernel launch");
+}
+
+static int do_effective(tmg_ctx *ctx, int64_t n, const int8_t *board, uint64_t *eff, hipStream_t s) {
+    const dim3 grid = env_grid(n), block(64 * TMG_WPB);
+    if (ctx->maxn == 128)
+        hipLaunchKernelGGL(tmg::effective_kernel<128>, grid, block, sizeof(tmg::Ws<128, false>) * TMG_WPB, s, ctx->P,
+                           n, board, eff);
+    else
+        hipLaunchKernelGGL(tmg::effective_kernel<512>, grid, block, sizeof(tmg::Ws<512, false>) * TMG_WPB, s, ctx->P,
+                           n, board, eff);
+    return hip_check(hipGetLastError(), "kernel launch");
+}
+
+static int check_call(tmg_ctx *ctx, int64_t n) {
     if (!ctx) return fail(-1, "null context");
     if (n < 0) return fail(-2, "negative batch size");
-    if (n == 0) return 0;
-    int dev = 0;
-    (void)hipGetDevice(&dev);
-    if (dev != ctx->device) {
-        int rc = hip_check(hipSetDevice(ctx->device), "hipSetDevice");
-        if (rc) return rc;
-    }
-    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-    if (ctx->maxn == 128)
-        return launch_all<128>(which, ctx, n, board, rng, timer, actions, reward, n_new, n_act, flags, eff, env_mask,
-                               trust_eff, autoreset, s);
-    return launch_all<512>(which, ctx, n, board, rng, timer, actions, reward, n_new, n_act, flags, eff, env_mask,
-                           trust_eff, autoreset, s);
+    return set_device(ctx);
 }
 
 extern "C" {
@@ -158,7 +187,12 @@ int tmg_create(tmg_ctx **out, int device, int rows, int cols, int colours, uint3
         tmg::build_sb_rows(P.R, P.C, rows);
         rc = hip_check(hipMalloc(&c->d_sbrows, sizeof rows), "hipMalloc");
         if (!rc) rc = hip_check(hipMemcpy(c->d_sbrows, rows, sizeof rows, hipMemcpyHostToDevice), "hipMemcpy");
-        if (rc) { (void)hipFree(c->d_jump); if (c->d_sbrows) (void)hipFree(c->d_sbrows); delete c; return rc; }
+        if (rc) {
+            (void)hipFree(c->d_jump);
+            if (c->d_sbrows) (void)hipFree(c->d_sbrows);
+            delete c;
+            return rc;
+        }
         P.sb_rows = c->d_sbrows;
     }
     *out = c;
@@ -176,8 +210,9 @@ int tmg_destroy(tmg_ctx *ctx) {
 int tmg_reset(tmg_ctx *ctx, int64_t n, int8_t *board, uint64_t *rng, int32_t *timer, uint64_t *eff,
               const uint8_t *env_mask, void *stream) {
     if (!board || !rng || !timer || !eff) return fail(-1, "null state buffer");
-    return dispatch(1, ctx, n, board, rng, timer, nullptr, nullptr, nullptr, nullptr, nullptr, eff, env_mask, 0, 0,
-                    stream);
+    int rc = check_call(ctx, n);
+    if (rc || n == 0) return rc;
+    return do_reset(ctx, n, board, rng, timer, eff, env_mask, reinterpret_cast<hipStream_t>(stream));
 }
 
 int tmg_step(tmg_ctx *ctx, int64_t n, int8_t *board, uint64_t *rng, int32_t *timer, const int32_t *actions,
@@ -185,14 +220,17 @@ int tmg_step(tmg_ctx *ctx, int64_t n, int8_t *board, uint64_t *rng, int32_t *tim
              int autoreset, void *stream) {
     if (!board || !rng || !timer || !actions || !reward || !n_new || !n_act || !flags || !eff)
         return fail(-1, "null buffer");
-    return dispatch(0, ctx, n, board, rng, timer, actions, reward, n_new, n_act, flags, eff, nullptr, trust_eff,
-                    autoreset, stream);
+    int rc = check_call(ctx, n);
+    if (rc || n == 0) return rc;
+    const StepArgs a{n, board, rng, timer, actions, reward, n_new, n_act, flags, eff, trust_eff, autoreset};
+    return do_step(ctx, a, reinterpret_cast<hipStream_t>(stream));
 }
 
 int tmg_effective(tmg_ctx *ctx, int64_t n, const int8_t *board, uint64_t *eff, void *stream) {
     if (!board || !eff) return fail(-1, "null buffer");
-    return dispatch(2, ctx, n, const_cast<int8_t *>(board), nullptr, nullptr, nullptr, nullptr, nullptr, nullptr,
-                    nullptr, eff, nullptr, 0, 0, stream);
+    int rc = check_call(ctx, n);
+    if (rc || n == 0) return rc;
+    return do_effective(ctx, n, board, eff, reinterpret_cast<hipStream_t>(stream));
 }
 
 #if TMG_STAMPS

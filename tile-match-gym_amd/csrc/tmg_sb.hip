@@ -365,7 +365,8 @@ __device__ __forceinline__ void sb_generate(const Params &P, WS &w, int lane, co
 // w.effw.
 template <int NB, bool CODD, class WS>
 __device__ __forceinline__ int sb_move(const Params &P, WS &w, int lane, const LaneJump &J, Rng &g,
-                                       const Cells<WS::NP> &cl, int p1, int p2, int &flags) {
+                                       const Cells<WS::NP> &cl, int p1, int p2, int &flags, int64_t e) {
+    (void)e;
     int8_t *col = w.brd;
     if (lane == 0) {                                     // swap_coords :355 (types are all 1)
         int8_t x = col[p1]; col[p1] = col[p2]; col[p2] = x;
@@ -382,6 +383,8 @@ __device__ __forceinline__ int sb_move(const Params &P, WS &w, int lane, const L
         elim += tot;                                     // R*C - nnz(type) after the resolve (:374)
         sb_gravity_refill<CODD>(P, w, lane, J, g, clr, tot, c);
     }
+    STAMP(e, 2);
     if (sb_ensure<NB, CODD>(P, w, lane, J, g, cl, c, false, true)) flags |= FL_SHUF;   // :381-391
+    STAMP(e, 3);
     return elim;
 }

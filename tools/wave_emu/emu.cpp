@@ -182,18 +182,23 @@ template <class F>
 static void body_thunk(void *p) { (*reinterpret_cast<F *>(p))(); }
 
 template <class F>
-static void run_blocks(int64_t n, size_t lds, F kernel) {
-    // one wave per block; the grid is padded to 8 XCD blocks like the host launcher does
-    int64_t nblocks = n;
-    if (TMG_XCD) nblocks = (nblocks + 7) & ~(int64_t)7;
+static void run_grid(int64_t nblocks, size_t lds, F kernel) {
     emu_grid_dim.x = (unsigned)nblocks;
     for (int64_t b = 0; b < nblocks; b++) {
-        std::vector<unsigned char> smem(lds);          // exactly sized: ASan catches any overrun
-        memset(smem.data(), 0xA5, lds);
+        std::vector<unsigned char> smem(lds ? lds : 1);    // exactly sized: ASan catches any overrun
+        memset(smem.data(), 0xA5, smem.size());
         g_smem = smem.data();
         emu_block_idx.x = (unsigned)b;
         run_wave(&body_thunk<F>, &kernel);
     }
+}
+
+// one wave per env; the grid is padded to 8 XCD blocks like the host launcher does
+template <class F>
+static void run_blocks(int64_t n, size_t lds, F kernel) {
+    int64_t nblocks = n;
+    if (TMG_XCD) nblocks = (nblocks + 7) & ~(int64_t)7;
+    run_grid(nblocks, lds, kernel);
 }
 
 static uint64_t g_sbrows[64 * 4];
@@ -214,32 +219,44 @@ static bool sb_ok(const tmg::Params &P) {
     return P.N <= 128 && P.C <= 63 && !(v && v[0] == '0');
 }
 
-// lean step (which 0) / reset (which 1) on scalar bitboards, as tmg_capi.hip's launch_sb
-template <int NB, bool CODD>
-static void run_sb(int which, const tmg::Params &P, int64_t n, int8_t *board, uint64_t *rng, int32_t *timer,
-                   const int32_t *actions, int32_t *reward, int32_t *n_new, int32_t *n_act, uint8_t *flags,
-                   uint64_t *eff, int trust_eff, int autoreset) {
-    if (which == 0)
-        run_blocks(n, sizeof(tmg::Ws<128, false>), [&] { tmg::step_kernel<128, false, NB, CODD>(P, n, board, rng, timer, actions, reward, n_new, n_act, flags, eff, trust_eff, autoreset); });
-    else
-        run_blocks(n, sizeof(tmg::Ws<128, false>), [&] { tmg::reset_kernel<128, NB, CODD>(P, n, board, rng, timer, eff, nullptr); });
+// step variants as tmg_capi.hip's do_step: one wave per env
+struct EmuStep {
+    const tmg::Params *P;
+    int64_t n;
+    int8_t *board; uint64_t *rng; int32_t *timer; const int32_t *actions;
+    int32_t *reward, *n_new, *n_act; uint8_t *flags; uint64_t *eff;
+    int trust_eff, autoreset;
+};
+
+template <int MAXN, bool GEN, int NB, bool CODD>
+static void emu_step_kernel(EmuStep &S) {
+    const tmg::Params &P = *S.P;
+    run_blocks(S.n, sizeof(tmg::Ws<MAXN, GEN>), [&] { tmg::step_kernel<MAXN, GEN, NB, CODD>(P, S.n, S.board, S.rng, S.timer, S.actions, S.reward, S.n_new, S.n_act, S.flags, S.eff, S.trust_eff, S.autoreset); });
 }
+
 template <bool CODD>
-static void run_sb_nb(int which, const tmg::Params &P, int64_t n, int8_t *board, uint64_t *rng, int32_t *timer,
-                      const int32_t *actions, int32_t *reward, int32_t *n_new, int32_t *n_act, uint8_t *flags,
-                      uint64_t *eff, int trust_eff, int autoreset) {
-    switch (tmg::sb_planes(P.k)) {
-    case 1: run_sb<1, CODD>(which, P, n, board, rng, timer, actions, reward, n_new, n_act, flags, eff, trust_eff, autoreset); break;
-    case 2: run_sb<2, CODD>(which, P, n, board, rng, timer, actions, reward, n_new, n_act, flags, eff, trust_eff, autoreset); break;
-    case 3: run_sb<3, CODD>(which, P, n, board, rng, timer, actions, reward, n_new, n_act, flags, eff, trust_eff, autoreset); break;
-    default: run_sb<4, CODD>(which, P, n, board, rng, timer, actions, reward, n_new, n_act, flags, eff, trust_eff, autoreset); break;
+static void emu_step_sb(EmuStep &S) {
+    switch (tmg::sb_planes(S.P->k)) {
+    case 1: emu_step_kernel<128, false, 1, CODD>(S); break;
+    case 2: emu_step_kernel<128, false, 2, CODD>(S); break;
+    case 3: emu_step_kernel<128, false, 3, CODD>(S); break;
+    default: emu_step_kernel<128, false, 4, CODD>(S); break;
     }
 }
-static void run_sb_any(int which, const tmg::Params &P, int64_t n, int8_t *board, uint64_t *rng, int32_t *timer,
-                       const int32_t *actions, int32_t *reward, int32_t *n_new, int32_t *n_act, uint8_t *flags,
-                       uint64_t *eff, int trust_eff, int autoreset) {
-    if (P.C & 1) run_sb_nb<true>(which, P, n, board, rng, timer, actions, reward, n_new, n_act, flags, eff, trust_eff, autoreset);
-    else run_sb_nb<false>(which, P, n, board, rng, timer, actions, reward, n_new, n_act, flags, eff, trust_eff, autoreset);
+
+template <int NB, bool CODD>
+static void emu_reset_kernel(const tmg::Params &P, int64_t n, int8_t *board, uint64_t *rng, int32_t *timer, uint64_t *eff) {
+    const int MAXN = 128;
+    run_blocks(n, sizeof(tmg::Ws<MAXN, false>), [&] { tmg::reset_kernel<MAXN, NB, CODD>(P, n, board, rng, timer, eff, nullptr); });
+}
+template <bool CODD>
+static void emu_reset_sb(const tmg::Params &P, int64_t n, int8_t *board, uint64_t *rng, int32_t *timer, uint64_t *eff) {
+    switch (tmg::sb_planes(P.k)) {
+    case 1: emu_reset_kernel<1, CODD>(P, n, board, rng, timer, eff); break;
+    case 2: emu_reset_kernel<2, CODD>(P, n, board, rng, timer, eff); break;
+    case 3: emu_reset_kernel<3, CODD>(P, n, board, rng, timer, eff); break;
+    default: emu_reset_kernel<4, CODD>(P, n, board, rng, timer, eff); break;
+    }
 }
 
 extern "C" {
@@ -249,19 +266,19 @@ int emu_step(int R, int C, int k, int smask, int moves, int64_t n, int8_t *board
              int trust_eff, int autoreset) {
     if (!g_jump_init) { tmg::build_jump_table(g_jump); g_jump_init = true; }
     tmg::Params P = make_params(R, C, k, smask, moves, g_jump);
+    EmuStep S;
+    S.P = &P; S.n = n; S.board = board; S.rng = rng; S.timer = timer; S.actions = actions; S.reward = reward;
+    S.n_new = n_new; S.n_act = n_act; S.flags = flags; S.eff = eff; S.trust_eff = trust_eff; S.autoreset = autoreset;
     const bool lean = smask == 0 && trust_eff;
     if (lean && sb_ok(P)) {
-        run_sb_any(0, P, n, board, rng, timer, actions, reward, n_new, n_act, flags, eff, trust_eff, autoreset);
+        if (P.C & 1) emu_step_sb<true>(S);
+        else emu_step_sb<false>(S);
     } else if (P.N <= 128) {
-        if (lean)
-            run_blocks(n, sizeof(tmg::Ws<128, false>), [&] { tmg::step_kernel<128, false>(P, n, board, rng, timer, actions, reward, n_new, n_act, flags, eff, trust_eff, autoreset); });
-        else
-            run_blocks(n, sizeof(tmg::Ws<128, true>), [&] { tmg::step_kernel<128, true>(P, n, board, rng, timer, actions, reward, n_new, n_act, flags, eff, trust_eff, autoreset); });
+        if (lean) emu_step_kernel<128, false, 0, false>(S);
+        else emu_step_kernel<128, true, 0, false>(S);
     } else {
-        if (lean)
-            run_blocks(n, sizeof(tmg::Ws<512, false>), [&] { tmg::step_kernel<512, false>(P, n, board, rng, timer, actions, reward, n_new, n_act, flags, eff, trust_eff, autoreset); });
-        else
-            run_blocks(n, sizeof(tmg::Ws<512, true>), [&] { tmg::step_kernel<512, true>(P, n, board, rng, timer, actions, reward, n_new, n_act, flags, eff, trust_eff, autoreset); });
+        if (lean) emu_step_kernel<512, false, 0, false>(S);
+        else emu_step_kernel<512, true, 0, false>(S);
     }
     return 0;
 }
@@ -270,12 +287,14 @@ int emu_reset(int R, int C, int k, int smask, int moves, int64_t n, int8_t *boar
               uint64_t *eff) {
     if (!g_jump_init) { tmg::build_jump_table(g_jump); g_jump_init = true; }
     tmg::Params P = make_params(R, C, k, smask, moves, g_jump);
-    if (sb_ok(P))
-        run_sb_any(1, P, n, board, rng, timer, nullptr, nullptr, nullptr, nullptr, nullptr, eff, 0, 0);
-    else if (P.N <= 128)
+    if (sb_ok(P)) {
+        if (P.C & 1) emu_reset_sb<true>(P, n, board, rng, timer, eff);
+        else emu_reset_sb<false>(P, n, board, rng, timer, eff);
+    } else if (P.N <= 128) {
         run_blocks(n, sizeof(tmg::Ws<128, false>), [&] { tmg::reset_kernel<128>(P, n, board, rng, timer, eff, nullptr); });
-    else
+    } else {
         run_blocks(n, sizeof(tmg::Ws<512, false>), [&] { tmg::reset_kernel<512>(P, n, board, rng, timer, eff, nullptr); });
+    }
     return 0;
 }
 
