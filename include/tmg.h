@@ -92,6 +92,29 @@ TMG_API int tmg_step(tmg_ctx *ctx, int64_t n, int8_t *board, uint64_t *rng, int3
  * is_move_effective board.py:735-787) as a bitmask, ignoring the timer. */
 TMG_API int tmg_effective(tmg_ctx *ctx, int64_t n, const int8_t *board, uint64_t *eff, void *stream);
 
+/* Output element types of tmg_onehot. */
+#define TMG_DTYPE_F32 0
+#define TMG_DTYPE_U8  1
+#define TMG_DTYPE_I32 2
+
+/* Replaces OneHotWrapper._one_hot_encode_board (src/tile_match_gym/wrappers.py:56-69)
+ * for n boards: out[n][C_oh][R][C] with C_oh = tmg_onehot_channels(ctx) =
+ * colours + #enabled specials.  Channel c < colours is (colour == c + 1); then
+ * one channel per enabled special in the order cookie, v-laser, h-laser, bomb
+ * (sorted(type id + 1), wrappers.py:39-46), set where the type equals it.
+ * The reference builds float64; out_dtype picks f32 / u8 / i32 (TMG_DTYPE_*).
+ * Asynchronous on `stream`. */
+TMG_API int tmg_onehot(tmg_ctx *ctx, int64_t n, const int8_t *board, void *out, int out_dtype, void *stream);
+TMG_API int tmg_onehot_channels(const tmg_ctx *ctx);
+
+/* Replaces utils.compute_num_states (src/tile_match_gym/utils/utils.py:6-26) on
+ * `device`: over all colours^(rows*cols) colourings of an all-normal board,
+ * num_line_free = boards with no colour line, num_playable = those that also
+ * have an effective move (the reference's two returned sums, in the order
+ * (playable, line_free)).  Needs rows*cols <= 16.  Synchronous. */
+TMG_API int tmg_count_states(int device, int rows, int cols, int colours, uint64_t *num_playable,
+                             uint64_t *num_line_free);
+
 /* Number of actions A = 2RC - R - C (tile_match_env.py:58) and mask words W. */
 TMG_API int tmg_num_actions(const tmg_ctx *ctx);
 TMG_API int tmg_mask_words(const tmg_ctx *ctx);

@@ -50,6 +50,7 @@ def lib():
             "orc_rng_shuffle": [P, I, P],
             "orc_env_reset_batch": [I, I, I, I, I64, P, P, P, P, I],
             "orc_env_step_batch": [I, I, I, I, I, I64, P, P, P, P, P, P, P, P, P, I, I],
+            "orc_count_states": [I, I, I, I, P, P],
         }
         for name, args in sig.items():
             fn = getattr(L, name)
@@ -161,6 +162,13 @@ def rng_shuffle(rng_words, n):
     out = np.zeros(n, np.int32)
     lib().orc_rng_shuffle(_p(rng), n, _p(out))
     return out, rng
+
+
+def count_states(R, C, k, threads=8):
+    """utils.compute_num_states restated (tmg_oracle.c): (playable, line_free)."""
+    out = np.zeros(2, np.uint64)
+    lib().orc_count_states(R, C, k, threads, out[0:].ctypes.data, out[1:].ctypes.data)
+    return int(out[0]), int(out[1])
 
 
 class OracleBatch:

@@ -691,6 +691,40 @@ EXPORT int orc_effective_mask(int R, int C, const int8_t *board, uint8_t *mask) 
     return any;
 }
 
+/* utils.compute_num_states / is_valid_state (src/tile_match_gym/utils/utils.py:6-26):
+ * every colouring of an all-normal board in itertools.product order (cell 0 the
+ * most significant digit), counted as (line-free with a possible move,
+ * line-free).  Uses this file's get_colour_lines and is_move_effective. */
+EXPORT int orc_count_states(int R, int C, int k, int threads, uint64_t *playable, uint64_t *line_free) {
+    const int N = R * C;
+    uint64_t total = 1;
+    for (int i = 0; i < N; i++) total *= (uint64_t)k;
+    uint64_t pl = 0, lf = 0;
+    if (threads > 0) omp_set_num_threads(threads);
+#pragma omp parallel for schedule(dynamic, 4096) reduction(+ : pl, lf)
+    for (int64_t idx = 0; idx < (int64_t)total; idx++) {
+        int8_t cells[2 * 64];
+        uint64_t v = (uint64_t)idx;
+        for (int p = N - 1; p >= 0; p--) { cells[p] = (int8_t)(1 + v % (uint64_t)k); v /= (uint64_t)k; cells[N + p] = 1; }
+        board_t b; bind(&b, R, C, k, 0, cells);
+        lines_t L; lines_init(&L);
+        get_colour_lines(&b, &L);
+        const int no_lines = L.n == 0;
+        lines_free(&L);
+        if (!no_lines) continue;
+        lf++;
+        int A = num_actions(R, C), r1, c1, r2, c2, any = 0;
+        for (int a = 0; a < A && !any; a++) {
+            action_coords(R, C, a, &r1, &c1, &r2, &c2);
+            any = is_move_effective(&b, r1, c1, r2, c2);
+        }
+        pl += (uint64_t)any;
+    }
+    *playable = pl;
+    *line_free = lf;
+    return 0;
+}
+
 EXPORT void orc_gravity(int R, int C, int8_t *board) {
     board_t b; bind(&b, R, C, 1, 0, board);
     gravity(&b);

@@ -1,0 +1,48 @@
+"""CPU checks of the §8(f) rows: the compute_num_states oracle against counts
+recorded from the reference itself (tests/golden/make_count_states.py), the
+checkpoint file format, and OneHotWrapper's channel selection."""
+import os
+
+import numpy as np
+import pytest
+
+from oracle import oracle as orc
+
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+def test_count_states_oracle_vs_reference():
+    d = np.load(os.path.join(GOLDEN, "fn_count_states.npz"))
+    assert len(d["shapes"]) >= 6
+    for (R, C, k), p, lf in zip(d["shapes"], d["playable"], d["line_free"]):
+        assert orc.count_states(int(R), int(C), int(k)) == (int(p), int(lf)), (R, C, k)
+
+
+def test_checkpoint_format_roundtrip(tmp_path):
+    from tile_match_gym_amd.vec_env import load_state, save_state
+    rs = np.random.default_rng(0)
+    n, R, C = 7, 5, 6
+    arrays = {"board": rs.integers(-1, 6, (n, 2, R, C)).astype(np.int8),
+              "rng": rs.integers(0, 2**63, (n, 5), dtype=np.int64).view(np.uint64),
+              "timer": rs.integers(0, 30, n).astype(np.int32),
+              "eff": rs.integers(0, 2**63, (n, 1), dtype=np.int64).view(np.uint64)}
+    cfg = {"num_rows": R, "num_cols": C, "num_colours": 5, "num_moves": 30, "colourless_specials": ["cookie"],
+           "colour_specials": ["bomb"], "num_envs": n, "autoreset": True}
+    p = tmp_path / "ck.npz"
+    save_state(p, arrays, cfg)
+    back, cfg2 = load_state(p)
+    for k in arrays:
+        assert back[k].dtype == arrays[k].dtype and np.array_equal(back[k], arrays[k])
+    assert {k: cfg2[k] for k in cfg} == cfg and cfg2["format"] == 1
+
+
+@pytest.mark.parametrize("cl,co,want", [
+    ([], [], []),
+    (["cookie"], [], [0]),
+    ([], ["bomb", "vertical_laser"], [3, 5]),
+    (["cookie"], ["horizontal_laser", "vertical_laser", "bomb"], [0, 3, 4, 5]),
+])
+def test_onehot_type_slices(cl, co, want):
+    """wrappers.py:37-46: kept type slices are sorted(id + 1), ids cookie -1, v 2, h 3, bomb 4."""
+    from tile_match_gym_amd.wrappers import _type_slices
+    assert list(_type_slices(cl, co)) == want

@@ -142,6 +142,13 @@ def test_generate_golden_gpu():
     (8, 8, 3, 15, 4096, 65),
     (5, 5, 3, 15, 4096, 65),
     (6, 7, 5, 1, 2048, 45),
+    # scalar-bitboard lean path (no specials, <= 128 cells): odd C, 1..4 colour planes, C = 63
+    (7, 5, 3, 0, 4096, 65),
+    (6, 9, 9, 0, 2048, 45),
+    (16, 8, 5, 0, 2048, 45),
+    (3, 4, 2, 0, 2048, 45),
+    (2, 63, 6, 0, 1024, 35),
+    (11, 11, 4, 0, 2048, 45),
 ])
 def test_oracle_parity_random_actions(cfg):
     """Batched random-action rollouts with autoreset vs the CPU oracle, every step."""

@@ -52,3 +52,32 @@ def test_trajectory_golden_emulated(emu_lib, name, autoreset, monkeypatch):
     monkeypatch.setenv("EMU_EPW", "1")      # one env per workgroup, as libtmg launches
     d = load_traj(name)
     assert replay_trajectory(d, _EmuBackend(emu, L, d), autoreset) > 0
+
+
+@pytest.mark.parametrize("cfg", [
+    # R, C, k, smask: the scalar-bitboard lean path (even/odd C, 1..4 colour planes,
+    # 128 cells, C = 63) and the general kernel with specials
+    (10, 10, 4, 0), (8, 8, 3, 0), (7, 5, 5, 0), (6, 9, 9, 0), (3, 4, 2, 0), (16, 8, 4, 0), (2, 63, 6, 0),
+    (11, 11, 4, 0), (10, 10, 4, 14), (8, 8, 3, 15), (5, 12, 6, 15),
+])
+def test_random_rollouts_emulated(emu_lib, cfg):
+    """Random-action rollouts with autoreset: emulated kernels vs the oracle, every field, every step."""
+    from oracle import oracle as orc
+    from tile_match_gym_amd.seeding import batch_rng_words
+    emu, L = emu_lib
+    R, C, k, sm = cfg
+    n, T = 12, 40
+    w = batch_rng_words(range(1000, 1000 + n))
+    e = emu.EmuBatch(L, R, C, k, sm, 7, w)
+    o = orc.OracleBatch(R, C, k, sm, 7, w)
+    e.reset()
+    o.reset()
+    rs = np.random.default_rng(R * 100 + C + sm)
+    A = 2 * R * C - R - C
+    for t in range(-1, T):
+        if t >= 0:
+            a = rs.integers(0, A, n).astype(np.int32)
+            e.step(a, True)
+            o.step(a, True)
+        for f in ("board", "rng", "eff", "reward", "flags", "timer", "n_new", "n_act"):
+            assert np.array_equal(getattr(e, f), getattr(o, f)), f"{cfg} step {t}: {f}"

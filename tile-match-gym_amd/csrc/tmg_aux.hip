@@ -1,0 +1,122 @@
+// tmg_aux.hip — the callers either side of the Board transition (SURVEY.md
+// §8(f)): the one-hot observation encoding of OneHotWrapper and the
+// brute-force state count of utils.compute_num_states.  Included by
+// tmg_capi.hip.  Both are plain HBM-streaming / integer kernels, one thread
+// per (env, cell) and one thread per run of boards respectively.
+
+namespace tmg {
+
+// OneHotWrapper._one_hot_encode_board (src/tile_match_gym/wrappers.py:56-69):
+// channels 0..k-1 = colour 1..k; then one channel per enabled special, in the
+// order of sorted(id + 1) over {cookie: -1, v-laser: 2, h-laser: 3, bomb: 4}
+// (wrappers.py:9-10, 39-46), i.e. cookie, v-laser, h-laser, bomb.  A colour-0
+// (colourless / empty) cell and a normal tile set no channel of their kind.
+// out: T [n][k + nsel][R][C].  One thread per cell: byte loads and each
+// channel's stores are coalesced across the wave.
+template <class T>
+__global__ __launch_bounds__(256) void onehot_kernel(int64_t n, int N, int k, int nsel, int4 sel,
+                                                     const int8_t *__restrict__ board, T *__restrict__ out) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= n * N) return;
+    const int64_t e = i / N;
+    const int p = (int)(i - e * N);
+    const int colour = board[e * 2 * N + p], type = board[e * 2 * N + N + p];
+    T *o = out + e * (int64_t)(k + nsel) * N + p;
+    for (int c = 0; c < k; c++) o[(int64_t)c * N] = (T)(colour == c + 1 ? 1 : 0);
+    const int ids[4] = {sel.x, sel.y, sel.z, sel.w};
+    for (int j = 0; j < nsel; j++) o[(int64_t)(k + j) * N] = (T)(type == ids[j] ? 1 : 0);
+}
+
+// utils.compute_num_states / is_valid_state (src/tile_match_gym/utils/utils.py:6-26):
+// over every colouring of an all-normal R x C board with colours 1..k (the
+// itertools.product order: cell 0 is the most significant digit), count the
+// boards with no colour line (get_colour_lines() == [], board.py:149-215) and,
+// of those, the ones with an effective move (possible_move, board.py:558-569).
+// A board is 4-bit nibbles of one uint64 (cell p at bits 4p..4p+3, N <= 16).
+// Each thread walks `per` consecutive boards with an odometer.
+struct CountGeo {
+    int R, C, N, k;
+    uint64_t ones;      // 0x1 in every cell nibble
+    uint64_t hmask;     // cells with c <= C-3
+    uint64_t vmask;     // cells with r <= R-3
+};
+
+__device__ __forceinline__ uint64_t nib_eq(uint64_t d, uint64_t ones) {   // bit 4p set iff nibble p of d is 0
+    return ~(d | (d >> 1) | (d >> 2) | (d >> 3)) & ones;
+}
+
+__device__ __forceinline__ bool has_line(const CountGeo &G, uint64_t x) {
+    const uint64_t eh = nib_eq(x ^ (x >> 4), G.ones);                    // cell p == cell p+1
+    const uint64_t ev = nib_eq(x ^ (x >> (4 * G.C)), G.ones);            // cell p == cell p+C
+    const uint64_t h3 = eh & (eh >> 4) & G.hmask;
+    const uint64_t v3 = ev & (ev >> (4 * G.C)) & G.vmask;
+    return (h3 | v3) != 0ULL;
+}
+
+__global__ __launch_bounds__(256) void count_states_kernel(CountGeo G, uint64_t total, uint64_t per,
+                                                           unsigned long long *counts) {
+    __shared__ unsigned long long sh[2][256];
+    const uint64_t t = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    const uint64_t b0 = t * per;
+    uint64_t playable = 0, linefree = 0;
+    if (b0 < total) {
+        // digits of b0, cell N-1 least significant; stored as colour - 1
+        uint64_t x = 0, v = b0;
+        for (int p = G.N - 1; p >= 0; p--) {
+            x |= (v % (uint64_t)G.k) << (4 * p);
+            v /= (uint64_t)G.k;
+        }
+        const uint64_t end = b0 + per < total ? b0 + per : total;
+        for (uint64_t b = b0; b < end; b++) {
+            if (!has_line(G, x)) {
+                linefree++;
+                bool mv = false;
+                // vertical swaps (p, p+C), then horizontal (p, p+1) with c <= C-2
+                for (int p = 0; p + G.C < G.N && !mv; p++) {
+                    const uint64_t d = ((x >> (4 * p)) ^ (x >> (4 * (p + G.C)))) & 0xF;
+                    mv = d && has_line(G, x ^ (d << (4 * p)) ^ (d << (4 * (p + G.C))));
+                }
+                for (int p = 0; p + 1 < G.N && !mv; p++) {
+                    if (p % G.C == G.C - 1) continue;
+                    const uint64_t d = ((x >> (4 * p)) ^ (x >> (4 * (p + 1)))) & 0xF;
+                    mv = d && has_line(G, x ^ (d << (4 * p)) ^ (d << (4 * (p + 1))));
+                }
+                playable += mv ? 1 : 0;
+            }
+            // odometer: next colouring
+            for (int p = G.N - 1; p >= 0; p--) {
+                const uint64_t dg = (x >> (4 * p)) & 0xF;
+                if (dg + 1 < (uint64_t)G.k) { x += 1ULL << (4 * p); break; }
+                x &= ~(0xFULL << (4 * p));
+            }
+        }
+    }
+    sh[0][threadIdx.x] = playable;
+    sh[1][threadIdx.x] = linefree;
+    __syncthreads();
+    for (int s = 128; s > 0; s >>= 1) {
+        if ((int)threadIdx.x < s) {
+            sh[0][threadIdx.x] += sh[0][threadIdx.x + s];
+            sh[1][threadIdx.x] += sh[1][threadIdx.x + s];
+        }
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        atomicAdd(&counts[0], sh[0][0]);
+        atomicAdd(&counts[1], sh[1][0]);
+    }
+}
+
+inline CountGeo make_count_geo(int R, int C, int k) {
+    CountGeo G;
+    G.R = R; G.C = C; G.N = R * C; G.k = k;
+    G.ones = G.hmask = G.vmask = 0;
+    for (int p = 0; p < G.N; p++) {
+        G.ones |= 1ULL << (4 * p);
+        if (p % C <= C - 3) G.hmask |= 1ULL << (4 * p);
+        if (p / C <= R - 3) G.vmask |= 1ULL << (4 * p);
+    }
+    return G;
+}
+
+}  // namespace tmg

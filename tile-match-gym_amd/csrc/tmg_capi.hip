@@ -8,6 +8,7 @@
 
 #include "tmg.h"
 #include "tmg_board.hip"
+#include "tmg_aux.hip"
 
 namespace {
 
@@ -231,6 +232,86 @@ int tmg_effective(tmg_ctx *ctx, int64_t n, const int8_t *board, uint64_t *eff, v
     int rc = check_call(ctx, n);
     if (rc || n == 0) return rc;
     return do_effective(ctx, n, board, eff, reinterpret_cast<hipStream_t>(stream));
+}
+
+// OneHotWrapper channel selection (wrappers.py:39-46): enabled specials as
+// type ids, in the order of sorted(id + 1)
+static int onehot_sel(uint32_t smask, int ids[4]) {
+    int n = 0;
+    if (smask & TMG_SPECIAL_COOKIE) ids[n++] = -1;
+    if (smask & TMG_SPECIAL_VLASER) ids[n++] = 2;
+    if (smask & TMG_SPECIAL_HLASER) ids[n++] = 3;
+    if (smask & TMG_SPECIAL_BOMB) ids[n++] = 4;
+    return n;
+}
+
+int tmg_onehot_channels(const tmg_ctx *ctx) {
+    if (!ctx) return -1;
+    int ids[4];
+    return ctx->P.k + onehot_sel((uint32_t)ctx->P.smask, ids);
+}
+
+int tmg_onehot(tmg_ctx *ctx, int64_t n, const int8_t *board, void *out, int out_dtype, void *stream) {
+    if (!board || !out) return fail(-1, "null buffer");
+    int rc = check_call(ctx, n);
+    if (rc || n == 0) return rc;
+    int ids[4] = {0, 0, 0, 0};
+    const int nsel = onehot_sel((uint32_t)ctx->P.smask, ids);
+    const int4 sel = make_int4(ids[0], ids[1], ids[2], ids[3]);
+    const int64_t cells = n * ctx->P.N;
+    const dim3 grid((unsigned)((cells + 255) / 256)), block(256);
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    switch (out_dtype) {
+    case TMG_DTYPE_F32:
+        hipLaunchKernelGGL(tmg::onehot_kernel<float>, grid, block, 0, s, n, ctx->P.N, ctx->P.k, nsel, sel, board, (float *)out);
+        break;
+    case TMG_DTYPE_U8:
+        hipLaunchKernelGGL(tmg::onehot_kernel<uint8_t>, grid, block, 0, s, n, ctx->P.N, ctx->P.k, nsel, sel, board, (uint8_t *)out);
+        break;
+    case TMG_DTYPE_I32:
+        hipLaunchKernelGGL(tmg::onehot_kernel<int32_t>, grid, block, 0, s, n, ctx->P.N, ctx->P.k, nsel, sel, board, (int32_t *)out);
+        break;
+    default:
+        return fail(-2, "unknown one-hot output dtype");
+    }
+    return hip_check(hipGetLastError(), "kernel launch");
+}
+
+int tmg_count_states(int device, int rows, int cols, int colours, uint64_t *num_playable, uint64_t *num_line_free) {
+    if (!num_playable || !num_line_free) return fail(-1, "null output pointer");
+    if (rows < 1 || cols < 1 || rows * cols > 16) return fail(-2, "count_states needs R*C <= 16");
+    if (colours < 1 || colours > 15) return fail(-2, "num_colours must be in [1, 15]");
+    double total_d = 1.0;
+    for (int i = 0; i < rows * cols; i++) total_d *= colours;
+    if (total_d > 1.1e12) return fail(-2, "too many boards to enumerate (k^(R*C) > 1.1e12)");
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return fail(-3, "no HIP device available");
+    if (device < 0 || device >= ndev) return fail(-3, "bad device index");
+    int rc = hip_check(hipSetDevice(device), "hipSetDevice");
+    if (rc) return rc;
+    uint64_t total = 1;
+    for (int i = 0; i < rows * cols; i++) total *= (uint64_t)colours;
+    const tmg::CountGeo G = tmg::make_count_geo(rows, cols, colours);
+    // >= ~256k threads when there is work for them, runs of >= 1 board
+    uint64_t per = total / (1ULL << 18);
+    if (per < 1) per = 1;
+    const uint64_t threads = (total + per - 1) / per;
+    unsigned long long *d = nullptr;
+    rc = hip_check(hipMalloc(&d, 2 * sizeof(unsigned long long)), "hipMalloc");
+    if (rc) return rc;
+    rc = hip_check(hipMemset(d, 0, 2 * sizeof(unsigned long long)), "hipMemset");
+    if (!rc) {
+        hipLaunchKernelGGL(tmg::count_states_kernel, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, 0, G, total,
+                           per, d);
+        rc = hip_check(hipGetLastError(), "kernel launch");
+    }
+    unsigned long long h[2] = {0, 0};
+    if (!rc) rc = hip_check(hipMemcpy(h, d, sizeof h, hipMemcpyDeviceToHost), "hipMemcpy");
+    (void)hipFree(d);
+    if (rc) return rc;
+    *num_playable = h[0];
+    *num_line_free = h[1];
+    return 0;
 }
 
 #if TMG_STAMPS

@@ -2,8 +2,11 @@
 
 Drop-in for akshilpatel/tile-match-gym's hot path: `TileMatchEnv` keeps the
 reference's Gymnasium reset/step API and spaces (tile_match_env.py:14-150),
-`TileMatchVecEnv` steps N boards per HIP launch.  Both run the transition in
-libtmg.so (csrc/, C ABI in include/tmg.h); there is no CPU fallback.
+`TileMatchVecEnv` steps N boards per HIP launch, `TileMatchVectorEnv` puts the
+Gymnasium vector-env surface on it.  The wrappers (`OneHotWrapper`,
+`ProportionRewardWrapper`, batched `VecOneHot`) and `compute_num_states`
+mirror the reference's wrappers.py / utils.py.  All run in libtmg.so (csrc/,
+C ABI in include/tmg.h); there is no CPU fallback.
 """
 from ._native import TmgError, load as load_native  # noqa: F401
 from .seeding import rng_words_from_seed, batch_rng_words  # noqa: F401
@@ -16,6 +19,15 @@ def __getattr__(name):  # lazy: importing torch-backed classes only when used
     if name == "TileMatchVecEnv":
         from .vec_env import TileMatchVecEnv
         return TileMatchVecEnv
+    if name == "TileMatchVectorEnv":
+        from .vector import TileMatchVectorEnv
+        return TileMatchVectorEnv
+    if name in ("OneHotWrapper", "ProportionRewardWrapper", "VecOneHot"):
+        from . import wrappers
+        return getattr(wrappers, name)
+    if name == "compute_num_states":
+        from .utils import compute_num_states
+        return compute_num_states
     raise AttributeError(name)
 
 

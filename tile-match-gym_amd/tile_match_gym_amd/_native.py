@@ -13,7 +13,9 @@ import os
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("TMG_LIB") or os.path.join(_HERE, "_lib", "libtmg.so")   # TMG_LIB: A/B another build
 EXPORTS = ("tmg_create", "tmg_destroy", "tmg_reset", "tmg_step", "tmg_effective",
-           "tmg_num_actions", "tmg_mask_words", "tmg_last_error", "tmg_abi_version")
+           "tmg_num_actions", "tmg_mask_words", "tmg_last_error", "tmg_abi_version",
+           "tmg_onehot", "tmg_onehot_channels", "tmg_count_states")
+DTYPE_F32, DTYPE_U8, DTYPE_I32 = 0, 1, 2
 ABI_VERSION = 1
 
 SPECIAL_BITS = {"cookie": 1, "vertical_laser": 2, "horizontal_laser": 4, "bomb": 8}
@@ -49,8 +51,12 @@ def load():
     L.tmg_last_error.argtypes = []
     L.tmg_last_error.restype = ctypes.c_char_p
     L.tmg_abi_version.argtypes = []
+    L.tmg_onehot.argtypes = [P, I64, P, P, I, P]
+    L.tmg_onehot_channels.argtypes = [P]
+    L.tmg_count_states.argtypes = [I, I, I, I, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64)]
     for name in ("tmg_create", "tmg_destroy", "tmg_reset", "tmg_step", "tmg_effective",
-                 "tmg_num_actions", "tmg_mask_words", "tmg_abi_version"):
+                 "tmg_num_actions", "tmg_mask_words", "tmg_abi_version", "tmg_onehot", "tmg_onehot_channels",
+                 "tmg_count_states"):
         getattr(L, name).restype = I
     if L.tmg_abi_version() != ABI_VERSION:
         raise TmgError("libtmg.so ABI version mismatch; rebuild it")
@@ -109,3 +115,17 @@ class Context:
 
     def effective(self, n, board, eff, stream):
         check(load().tmg_effective(self._h, int(n), board, eff, stream))
+
+    def onehot_channels(self) -> int:
+        return load().tmg_onehot_channels(self._h)
+
+    def onehot(self, n, board, out, out_dtype, stream):
+        check(load().tmg_onehot(self._h, int(n), board, out, int(out_dtype), stream))
+
+
+def count_states(device_index: int, rows: int, cols: int, colours: int):
+    """(num_playable, num_line_free) over all colourings (tmg_count_states)."""
+    a, b = ctypes.c_uint64(0), ctypes.c_uint64(0)
+    check(load().tmg_count_states(int(device_index), int(rows), int(cols), int(colours), ctypes.byref(a),
+                                  ctypes.byref(b)))
+    return int(a.value), int(b.value)

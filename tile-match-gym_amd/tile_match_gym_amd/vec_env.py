@@ -13,11 +13,35 @@ a seed, tile_match_env.py:84-87); reward/flags describe the final move,
 """
 from __future__ import annotations
 
+import json
+
 import numpy as np
 import torch
 
 from . import _native
 from .seeding import batch_rng_words, rng_words_from_seed
+
+CHECKPOINT_FORMAT = 1
+_STATE_ARRAYS = ("board", "rng", "timer", "eff")
+
+
+def save_state(path, arrays: dict, config: dict) -> None:
+    """Write a batched-env checkpoint: the four state arrays (include/tmg.h
+    layout) plus the env config as JSON, in one .npz (no pickled objects)."""
+    meta = dict(config, format=CHECKPOINT_FORMAT)
+    np.savez(path, config=np.array(json.dumps(meta, sort_keys=True)),
+             **{k: np.ascontiguousarray(arrays[k]) for k in _STATE_ARRAYS})
+
+
+def load_state(path):
+    """(arrays, config) of a checkpoint written by save_state (numpy.load with
+    allow_pickle=False)."""
+    with np.load(path, allow_pickle=False) as z:
+        config = json.loads(str(z["config"]))
+        if config.get("format") != CHECKPOINT_FORMAT:
+            raise ValueError(f"unsupported checkpoint format {config.get('format')!r}")
+        arrays = {k: z[k].copy() for k in _STATE_ARRAYS}
+    return arrays, config
 
 
 def _ptr(t: torch.Tensor):
@@ -124,6 +148,52 @@ class TileMatchVecEnv:
 
     def rng_words(self) -> np.ndarray:
         return self.rng.cpu().numpy().view(np.uint64)
+
+    # ------------------------------------------------------- checkpoint/restore
+    def config(self) -> dict:
+        return {"num_rows": self.num_rows, "num_cols": self.num_cols, "num_colours": self.num_colours,
+                "num_moves": self.num_moves, "colourless_specials": self.colourless_specials,
+                "colour_specials": self.colour_specials, "num_envs": self.num_envs, "autoreset": self.autoreset}
+
+    def state_dict(self) -> dict:
+        """Host copy of the whole batched state: boards, the exact PCG64 stream
+        position of every env (incl. numpy's buffered half-word), timers and the
+        effective-action masks; restoring it continues every trajectory
+        bit-exactly."""
+        torch.cuda.synchronize(self.device)
+        return {"board": self.board.cpu().numpy(), "rng": self.rng_words().copy(),
+                "timer": self.timer.cpu().numpy(), "eff": self.eff.cpu().numpy().view(np.uint64).copy(),
+                "eff_valid": self._eff_valid, "config": self.config()}
+
+    def load_state_dict(self, sd: dict) -> None:
+        cfg = sd["config"]
+        mine = self.config()
+        def norm(v):
+            return list(v) if isinstance(v, (list, tuple)) else v
+
+        for k in ("num_rows", "num_cols", "num_colours", "num_moves", "colourless_specials", "colour_specials",
+                  "num_envs"):
+            if norm(cfg[k]) != norm(mine[k]):
+                raise ValueError(f"checkpoint {k}={cfg[k]!r} does not match this env ({mine[k]!r})")
+        self.board.copy_(torch.from_numpy(np.ascontiguousarray(sd["board"], dtype=np.int8)))
+        self.rng.copy_(torch.from_numpy(np.ascontiguousarray(sd["rng"], dtype=np.uint64).view(np.int64)))
+        self.timer.copy_(torch.from_numpy(np.ascontiguousarray(sd["timer"], dtype=np.int32)))
+        self.eff.copy_(torch.from_numpy(np.ascontiguousarray(sd["eff"], dtype=np.uint64).view(np.int64)))
+        self._eff_valid = bool(sd.get("eff_valid", True))
+
+    def save(self, path) -> None:
+        sd = self.state_dict()
+        cfg = dict(sd["config"], eff_valid=sd["eff_valid"])
+        save_state(path, sd, cfg)
+
+    @classmethod
+    def load(cls, path, device=None) -> "TileMatchVecEnv":
+        arrays, cfg = load_state(path)
+        env = cls(cfg["num_envs"], cfg["num_rows"], cfg["num_cols"], cfg["num_colours"], cfg["num_moves"],
+                  cfg["colourless_specials"], cfg["colour_specials"], seeds=range(cfg["num_envs"]), device=device,
+                  autoreset=cfg["autoreset"])
+        env.load_state_dict(dict(arrays, config=cfg, eff_valid=cfg.get("eff_valid", True)))
+        return env
 
     def close(self):
         self.ctx.close()
