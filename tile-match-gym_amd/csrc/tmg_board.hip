@@ -1317,9 +1317,12 @@ __device__ __forceinline__ void store_rng(uint64_t *p, const Rng &g, int lane) {
 
 // TileMatchEnv.step for env e on one wave (tile_match_env.py:93-112).
 // GEN=false: lean variant for boards that can hold no special (no specials
-// enabled, cached effective mask trusted).  SBNB > 0 (lean, <= 128 cells):
-// the scalar-bitboard path of tmg_sb.hip with SBNB colour planes; CODD = C
-// is odd.
+// enabled, cached effective mask trusted).  SBNB > 0 (<= 128 cells): the
+// scalar-bitboard path of tmg_sb.hip with SBNB colour planes (the move in the
+// lean variant, board generation in both); CODD = C is odd.  autoreset: 1
+// regenerates a finished board here, 2 leaves it to a following reset_kernel
+// launch masked by FL_RESET (the 512-cell kernels: the reset kernel's
+// occupancy is far higher than the general step kernel's).
 template <int MAXN, bool GEN, int SBNB, bool CODD>
 __device__ __forceinline__ void step_env(
     const Params &P, Ws<MAXN, GEN> &w, int lane, int64_t e, int8_t *__restrict__ board, uint64_t *__restrict__ rng, int32_t *__restrict__ timer,
@@ -1375,18 +1378,20 @@ __device__ __forceinline__ void step_env(
     bool changed = false;
     STAMP(e, 1);
     if (effective) {
-        if constexpr (SBNB > 0) elim = sb_move<SBNB, CODD>(P, w, lane, J, g, cl, p1, p2, flags, e);
+        if constexpr (SBNB > 0 && !GEN) elim = sb_move<SBNB, CODD>(P, w, lane, J, g, cl, p1, p2, flags, e);
         else elim = board_move(P, w, lane, J, g, cl, p1, p2, flags, nn, na, e);
         changed = true;
     }
     STAMP(e, 4);
     int tnew = t1;
     if (done && autoreset) {                                                // reset() without a seed
-        if constexpr (SBNB > 0) sb_generate<SBNB, CODD>(P, w, lane, J, g, cl);
-        else generate_board(P, w, lane, J, g, cl);
+        if (autoreset == 1) {
+            if constexpr (SBNB > 0) sb_generate<SBNB, CODD>(P, w, lane, J, g, cl);
+            else generate_board(P, w, lane, J, g, cl);
+            changed = true;
+        }                                      // autoreset == 2: reset_kernel regenerates FL_RESET envs next
         tnew = 0;
         flags |= FL_RESET;
-        changed = true;
     }
     STAMP(e, 5);
     if (changed) {
@@ -1435,7 +1440,7 @@ template <int MAXN, int SBNB = 0, bool CODD = false>
 __global__ TMG_LAUNCH_BOUNDS void reset_kernel(Params P, int64_t n, int8_t *__restrict__ board,
                                                              uint64_t *__restrict__ rng, int32_t *__restrict__ timer,
                                                              uint64_t *__restrict__ eff,
-                                                             const uint8_t *__restrict__ env_mask) {
+                                                             const uint8_t *__restrict__ env_mask, int mask_bits) {
     TMG_SMEM_DECL(smem);
     using WS = Ws<MAXN, false>;
     const int lane = threadIdx.x & 63;
@@ -1443,7 +1448,7 @@ __global__ TMG_LAUNCH_BOUNDS void reset_kernel(Params P, int64_t n, int8_t *__re
     WS &w = reinterpret_cast<WS *>(smem)[wv];
     const int64_t e = wg_env0() + wv;
     if (e >= n) return;
-    if (env_mask && !__builtin_amdgcn_readfirstlane((int)env_mask[e])) return;
+    if (env_mask && !(__builtin_amdgcn_readfirstlane((int)env_mask[e]) & mask_bits)) return;
     const int N = P.N, W = P.W;
     Rng g = load_rng(rng + e * 5);
     const LaneJump J = load_jump(P, lane, g);

@@ -58,30 +58,30 @@ static void launch_step(dim3 grid, hipStream_t s, const Params &P, const StepArg
 
 template <int MAXN, int NB, bool CODD>
 static void launch_reset(dim3 grid, hipStream_t s, const Params &P, int64_t n, int8_t *board, uint64_t *rng,
-                         int32_t *timer, uint64_t *eff, const uint8_t *env_mask) {
+                         int32_t *timer, uint64_t *eff, const uint8_t *env_mask, int mask_bits) {
     const size_t lds = sizeof(tmg::Ws<MAXN, false>) * TMG_WPB;
     hipLaunchKernelGGL((tmg::reset_kernel<MAXN, NB, CODD>), grid, dim3(64 * TMG_WPB), lds, s, P, n, board, rng, timer,
-                       eff, env_mask);
+                       eff, env_mask, mask_bits);
 }
 
 // scalar-bitboard variants: NB colour planes, C odd or even
-template <bool CODD>
+template <bool GEN, bool CODD>
 static void launch_step_sb(dim3 grid, hipStream_t s, const Params &P, const StepArgs &a) {
     switch (tmg::sb_planes(P.k)) {
-    case 1: launch_step<128, false, 1, CODD>(grid, s, P, a); break;
-    case 2: launch_step<128, false, 2, CODD>(grid, s, P, a); break;
-    case 3: launch_step<128, false, 3, CODD>(grid, s, P, a); break;
-    default: launch_step<128, false, 4, CODD>(grid, s, P, a); break;
+    case 1: launch_step<128, GEN, 1, CODD>(grid, s, P, a); break;
+    case 2: launch_step<128, GEN, 2, CODD>(grid, s, P, a); break;
+    case 3: launch_step<128, GEN, 3, CODD>(grid, s, P, a); break;
+    default: launch_step<128, GEN, 4, CODD>(grid, s, P, a); break;
     }
 }
 template <bool CODD>
 static void launch_reset_sb(dim3 grid, hipStream_t s, const Params &P, int64_t n, int8_t *board, uint64_t *rng,
-                            int32_t *timer, uint64_t *eff, const uint8_t *env_mask) {
+                            int32_t *timer, uint64_t *eff, const uint8_t *env_mask, int mask_bits) {
     switch (tmg::sb_planes(P.k)) {
-    case 1: launch_reset<128, 1, CODD>(grid, s, P, n, board, rng, timer, eff, env_mask); break;
-    case 2: launch_reset<128, 2, CODD>(grid, s, P, n, board, rng, timer, eff, env_mask); break;
-    case 3: launch_reset<128, 3, CODD>(grid, s, P, n, board, rng, timer, eff, env_mask); break;
-    default: launch_reset<128, 4, CODD>(grid, s, P, n, board, rng, timer, eff, env_mask); break;
+    case 1: launch_reset<128, 1, CODD>(grid, s, P, n, board, rng, timer, eff, env_mask, mask_bits); break;
+    case 2: launch_reset<128, 2, CODD>(grid, s, P, n, board, rng, timer, eff, env_mask, mask_bits); break;
+    case 3: launch_reset<128, 3, CODD>(grid, s, P, n, board, rng, timer, eff, env_mask, mask_bits); break;
+    default: launch_reset<128, 4, CODD>(grid, s, P, n, board, rng, timer, eff, env_mask, mask_bits); break;
     }
 }
 
@@ -99,41 +99,53 @@ static int set_device(tmg_ctx *ctx) {
     return 0;
 }
 
-static int do_step(tmg_ctx *ctx, const StepArgs &a, hipStream_t s) {
+static int do_reset(tmg_ctx *ctx, int64_t n, int8_t *board, uint64_t *rng, int32_t *timer, uint64_t *eff,
+                    const uint8_t *env_mask, int mask_bits, hipStream_t s) {
+    const Params &P = ctx->P;
+    const dim3 grid = env_grid(n);
+    if (ctx->maxn == 128) {
+        if (ctx->sb) {
+            if (P.C & 1) launch_reset_sb<true>(grid, s, P, n, board, rng, timer, eff, env_mask, mask_bits);
+            else launch_reset_sb<false>(grid, s, P, n, board, rng, timer, eff, env_mask, mask_bits);
+        } else {
+            launch_reset<128, 0, false>(grid, s, P, n, board, rng, timer, eff, env_mask, mask_bits);
+        }
+    } else {
+        launch_reset<512, 0, false>(grid, s, P, n, board, rng, timer, eff, env_mask, mask_bits);
+    }
+    return hip_check(hipGetLastError(), "kernel launch");
+}
+
+static int do_step(tmg_ctx *ctx, StepArgs a, hipStream_t s) {
     const Params &P = ctx->P;
     const bool lean = P.smask == 0 && a.trust_eff;
     const dim3 grid = env_grid(a.n);
+    a.autoreset = a.autoreset ? 1 : 0;
     if (ctx->maxn == 128) {
-        if (lean && ctx->sb) {
-            if (P.C & 1) launch_step_sb<true>(grid, s, P, a);
-            else launch_step_sb<false>(grid, s, P, a);
+        if (ctx->sb) {
+            if (lean) {
+                if (P.C & 1) launch_step_sb<false, true>(grid, s, P, a);
+                else launch_step_sb<false, false>(grid, s, P, a);
+            } else {
+                if (P.C & 1) launch_step_sb<true, true>(grid, s, P, a);
+                else launch_step_sb<true, false>(grid, s, P, a);
+            }
         } else if (lean) {
             launch_step<128, false, 0, false>(grid, s, P, a);
         } else {
             launch_step<128, true, 0, false>(grid, s, P, a);
         }
-    } else {
-        if (lean) launch_step<512, false, 0, false>(grid, s, P, a);
-        else launch_step<512, true, 0, false>(grid, s, P, a);
+        return hip_check(hipGetLastError(), "kernel launch");
     }
-    return hip_check(hipGetLastError(), "kernel launch");
-}
-
-static int do_reset(tmg_ctx *ctx, int64_t n, int8_t *board, uint64_t *rng, int32_t *timer, uint64_t *eff,
-                    const uint8_t *env_mask, hipStream_t s) {
-    const Params &P = ctx->P;
-    const dim3 grid = env_grid(n);
-    if (ctx->maxn == 128) {
-        if (ctx->sb) {
-            if (P.C & 1) launch_reset_sb<true>(grid, s, P, n, board, rng, timer, eff, env_mask);
-            else launch_reset_sb<false>(grid, s, P, n, board, rng, timer, eff, env_mask);
-        } else {
-            launch_reset<128, 0, false>(grid, s, P, n, board, rng, timer, eff, env_mask);
-        }
-    } else {
-        launch_reset<512, 0, false>(grid, s, P, n, board, rng, timer, eff, env_mask);
-    }
-    return hip_check(hipGetLastError(), "kernel launch");
+    // 512-cell kernels: finished boards are regenerated by a reset_kernel launch
+    // masked by FL_RESET, which runs at several times the step kernel's occupancy
+    const int deferred = a.autoreset;
+    if (deferred) a.autoreset = 2;
+    if (lean) launch_step<512, false, 0, false>(grid, s, P, a);
+    else launch_step<512, true, 0, false>(grid, s, P, a);
+    int rc = hip_check(hipGetLastError(), "kernel launch");
+    if (rc || !deferred) return rc;
+    return do_reset(ctx, a.n, a.board, a.rng, a.timer, a.eff, a.flags, tmg::FL_RESET, s);
 }
 
 static int do_effective(tmg_ctx *ctx, int64_t n, const int8_t *board, uint64_t *eff, hipStream_t s) {
@@ -213,7 +225,7 @@ int tmg_reset(tmg_ctx *ctx, int64_t n, int8_t *board, uint64_t *rng, int32_t *ti
     if (!board || !rng || !timer || !eff) return fail(-1, "null state buffer");
     int rc = check_call(ctx, n);
     if (rc || n == 0) return rc;
-    return do_reset(ctx, n, board, rng, timer, eff, env_mask, reinterpret_cast<hipStream_t>(stream));
+    return do_reset(ctx, n, board, rng, timer, eff, env_mask, 0xFF, reinterpret_cast<hipStream_t>(stream));
 }
 
 int tmg_step(tmg_ctx *ctx, int64_t n, int8_t *board, uint64_t *rng, int32_t *timer, const int32_t *actions,

@@ -234,28 +234,42 @@ static void emu_step_kernel(EmuStep &S) {
     run_blocks(S.n, sizeof(tmg::Ws<MAXN, GEN>), [&] { tmg::step_kernel<MAXN, GEN, NB, CODD>(P, S.n, S.board, S.rng, S.timer, S.actions, S.reward, S.n_new, S.n_act, S.flags, S.eff, S.trust_eff, S.autoreset); });
 }
 
-template <bool CODD>
+template <bool GEN, bool CODD>
 static void emu_step_sb(EmuStep &S) {
     switch (tmg::sb_planes(S.P->k)) {
-    case 1: emu_step_kernel<128, false, 1, CODD>(S); break;
-    case 2: emu_step_kernel<128, false, 2, CODD>(S); break;
-    case 3: emu_step_kernel<128, false, 3, CODD>(S); break;
-    default: emu_step_kernel<128, false, 4, CODD>(S); break;
+    case 1: emu_step_kernel<128, GEN, 1, CODD>(S); break;
+    case 2: emu_step_kernel<128, GEN, 2, CODD>(S); break;
+    case 3: emu_step_kernel<128, GEN, 3, CODD>(S); break;
+    default: emu_step_kernel<128, GEN, 4, CODD>(S); break;
     }
 }
 
-template <int NB, bool CODD>
-static void emu_reset_kernel(const tmg::Params &P, int64_t n, int8_t *board, uint64_t *rng, int32_t *timer, uint64_t *eff) {
-    const int MAXN = 128;
-    run_blocks(n, sizeof(tmg::Ws<MAXN, false>), [&] { tmg::reset_kernel<MAXN, NB, CODD>(P, n, board, rng, timer, eff, nullptr); });
+template <int MAXN, int NB, bool CODD>
+static void emu_reset_kernel(const tmg::Params &P, int64_t n, int8_t *board, uint64_t *rng, int32_t *timer, uint64_t *eff,
+                             const uint8_t *mask, int bits) {
+    run_blocks(n, sizeof(tmg::Ws<MAXN, false>), [&] { tmg::reset_kernel<MAXN, NB, CODD>(P, n, board, rng, timer, eff, mask, bits); });
 }
 template <bool CODD>
-static void emu_reset_sb(const tmg::Params &P, int64_t n, int8_t *board, uint64_t *rng, int32_t *timer, uint64_t *eff) {
+static void emu_reset_sb(const tmg::Params &P, int64_t n, int8_t *board, uint64_t *rng, int32_t *timer, uint64_t *eff,
+                         const uint8_t *mask, int bits) {
     switch (tmg::sb_planes(P.k)) {
-    case 1: emu_reset_kernel<1, CODD>(P, n, board, rng, timer, eff); break;
-    case 2: emu_reset_kernel<2, CODD>(P, n, board, rng, timer, eff); break;
-    case 3: emu_reset_kernel<3, CODD>(P, n, board, rng, timer, eff); break;
-    default: emu_reset_kernel<4, CODD>(P, n, board, rng, timer, eff); break;
+    case 1: emu_reset_kernel<128, 1, CODD>(P, n, board, rng, timer, eff, mask, bits); break;
+    case 2: emu_reset_kernel<128, 2, CODD>(P, n, board, rng, timer, eff, mask, bits); break;
+    case 3: emu_reset_kernel<128, 3, CODD>(P, n, board, rng, timer, eff, mask, bits); break;
+    default: emu_reset_kernel<128, 4, CODD>(P, n, board, rng, timer, eff, mask, bits); break;
+    }
+}
+
+// as tmg_capi.hip's do_reset
+static void emu_do_reset(const tmg::Params &P, int64_t n, int8_t *board, uint64_t *rng, int32_t *timer, uint64_t *eff,
+                         const uint8_t *mask, int bits) {
+    if (sb_ok(P)) {
+        if (P.C & 1) emu_reset_sb<true>(P, n, board, rng, timer, eff, mask, bits);
+        else emu_reset_sb<false>(P, n, board, rng, timer, eff, mask, bits);
+    } else if (P.N <= 128) {
+        emu_reset_kernel<128, 0, false>(P, n, board, rng, timer, eff, mask, bits);
+    } else {
+        emu_reset_kernel<512, 0, false>(P, n, board, rng, timer, eff, mask, bits);
     }
 }
 
@@ -270,16 +284,24 @@ int emu_step(int R, int C, int k, int smask, int moves, int64_t n, int8_t *board
     S.P = &P; S.n = n; S.board = board; S.rng = rng; S.timer = timer; S.actions = actions; S.reward = reward;
     S.n_new = n_new; S.n_act = n_act; S.flags = flags; S.eff = eff; S.trust_eff = trust_eff; S.autoreset = autoreset;
     const bool lean = smask == 0 && trust_eff;
-    if (lean && sb_ok(P)) {
-        if (P.C & 1) emu_step_sb<true>(S);
-        else emu_step_sb<false>(S);
-    } else if (P.N <= 128) {
-        if (lean) emu_step_kernel<128, false, 0, false>(S);
-        else emu_step_kernel<128, true, 0, false>(S);
-    } else {
-        if (lean) emu_step_kernel<512, false, 0, false>(S);
-        else emu_step_kernel<512, true, 0, false>(S);
+    S.autoreset = autoreset ? 1 : 0;
+    if (P.N <= 128) {
+        if (sb_ok(P)) {
+            if (lean) { if (P.C & 1) emu_step_sb<false, true>(S); else emu_step_sb<false, false>(S); }
+            else { if (P.C & 1) emu_step_sb<true, true>(S); else emu_step_sb<true, false>(S); }
+        } else if (lean) {
+            emu_step_kernel<128, false, 0, false>(S);
+        } else {
+            emu_step_kernel<128, true, 0, false>(S);
+        }
+        return 0;
     }
+    // 512-cell kernels: deferred regeneration by a reset launch masked by FL_RESET
+    const int deferred = S.autoreset;
+    if (deferred) S.autoreset = 2;
+    if (lean) emu_step_kernel<512, false, 0, false>(S);
+    else emu_step_kernel<512, true, 0, false>(S);
+    if (deferred) emu_do_reset(P, n, board, rng, timer, eff, flags, tmg::FL_RESET);
     return 0;
 }
 
@@ -287,14 +309,7 @@ int emu_reset(int R, int C, int k, int smask, int moves, int64_t n, int8_t *boar
               uint64_t *eff) {
     if (!g_jump_init) { tmg::build_jump_table(g_jump); g_jump_init = true; }
     tmg::Params P = make_params(R, C, k, smask, moves, g_jump);
-    if (sb_ok(P)) {
-        if (P.C & 1) emu_reset_sb<true>(P, n, board, rng, timer, eff);
-        else emu_reset_sb<false>(P, n, board, rng, timer, eff);
-    } else if (P.N <= 128) {
-        run_blocks(n, sizeof(tmg::Ws<128, false>), [&] { tmg::reset_kernel<128>(P, n, board, rng, timer, eff, nullptr); });
-    } else {
-        run_blocks(n, sizeof(tmg::Ws<512, false>), [&] { tmg::reset_kernel<512>(P, n, board, rng, timer, eff, nullptr); });
-    }
+    emu_do_reset(P, n, board, rng, timer, eff, nullptr, 0xFF);
     return 0;
 }
 
