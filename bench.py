@@ -3,7 +3,9 @@
 
     python bench.py --gpus N --steps K --warmup W [--config c2|c3|c5]
 
-One "step" = one TileMatchEnv.step for every env of the shard (one HIP launch),
+One "step" = one TileMatchEnv.step for every env of the shard (one HIP launch
+per env group; `--groups` groups run on separate HIP streams so one group's
+launch tail overlaps the next group's launch — same boards, same work),
 uniform random actions pre-staged in HBM, autoreset on (num_moves = 30, so
 every 30th step also regenerates every board).  Each rank steps its own
 contiguous shard of envs (seed = global env index); there is no collective on
@@ -91,6 +93,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=30)
     ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
     ap.add_argument("--boards", type=int, default=0, help="override boards per GPU")
+    ap.add_argument("--groups", type=int, default=3,
+                    help="env groups per GPU, each stepped on its own HIP stream (TileMatchVecEnv(groups=))")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
 
@@ -99,8 +103,10 @@ def main():
     dist = None
     if world > 1:
         import torch.distributed as dist
-        torch.cuda.set_device(local_rank)
-        dist.init_process_group("nccl")
+        # one process per GPU; TMG_DIST_BACKEND=gloo rehearses the N>1 path with
+        # several ranks on one device (RCCL refuses duplicate GPUs)
+        torch.cuda.set_device(local_rank % torch.cuda.device_count())
+        dist.init_process_group(os.environ.get("TMG_DIST_BACKEND", "nccl"))
     else:
         torch.cuda.set_device(0)
     dev = torch.device("cuda", torch.cuda.current_device())
@@ -110,30 +116,36 @@ def main():
     if args.boards:
         nb = args.boards
     moves = 30
-    env = TileMatchVecEnv(nb, R, C, k, moves, cl, co, seeds=shard_seeds(rank, nb), device=dev, autoreset=True)
+    env = TileMatchVecEnv(nb, R, C, k, moves, cl, co, seeds=shard_seeds(rank, nb), device=dev, autoreset=True,
+                          groups=args.groups)
     A = env.num_actions
     T = 300
     acts = torch.from_numpy(synthetic_actions(shard_range(rank, nb), T, A)).to(dev)
     env.reset()
     for t in range(args.warmup):
         env.step_raw(acts[t % T])
+    env.join()
     torch.cuda.synchronize()
 
-    stream = torch.cuda.current_stream()
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    # HIP events on the stream the first env group's kernels are launched on,
+    # bracketing the timed region: its back-to-back launches' average duration
+    # (the dominant kernel's per-launch time for the roofline)
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
+    env.record(ev0)
     for i in range(args.steps):
-        ev[i][0].record(stream)
         env.step_raw(acts[(args.warmup + i) % T])
-        ev[i][1].record(stream)
+    env.record(ev1)
+    env.join()
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
     el = time.perf_counter() - t0
-    kern_ms = sum(a.elapsed_time(b) for a, b in ev) / max(1, args.steps)
+    kern_ms = ev0.elapsed_time(ev1) / max(1, args.steps)
+    launch_envs = env._ranges[0][1] - env._ranges[0][0]
     flags = env.flags.cpu().numpy()
     assert not (flags & 0xC0).any(), "error/overflow flag raised during the bench"
     el = max_over_ranks(el, dist, dev)
@@ -143,7 +155,7 @@ def main():
         total = nb * world * args.steps
         value = total / el
         bpu = algorithmic_bytes_per_env_step(R, C)
-        achieved = bpu * nb / (kern_ms * 1e-3) / 1e9
+        achieved = bpu * launch_envs / (kern_ms * 1e-3) / 1e9
         smask = (1 if "cookie" in cl else 0) | (2 if "vertical_laser" in co else 0) | \
                 (4 if "horizontal_laser" in co else 0) | (8 if "bomb" in co else 0)
         cpu = None if (args.no_cpu_baseline or world > 1) else cpu_baseline(R, C, k, smask, moves)
@@ -162,10 +174,13 @@ def main():
             "data": "synthetic (uniform random actions, counter-based per (step, global env); seeds = global env index)",
             "config": {"workload": f"{args.config}: {desc}, num_moves=30, autoreset",
                        "boards_per_gpu": nb, "rows": R, "cols": C, "colours": k,
-                       "specials": cl + co, "parallelism": f"dp{world} (independent env shards, no collective)"},
+                       "specials": cl + co, "env_groups_per_gpu": env.groups,
+                       "parallelism": f"dp{world} (independent env shards, no collective)"},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 6), "traffic": load_traffic(args.config),
-                         "kernel_ms_per_launch": round(kern_ms, 4), "algorithmic_bytes_per_env_step": bpu},
+                         "kernel_ms_per_launch": round(kern_ms, 4), "envs_per_launch": launch_envs,
+                         "algorithmic_bytes_per_env_step": bpu,
+                         "job_gbs": round(bpu * nb * args.steps / el / 1e9, 2)},
             "cpu_baseline": cpu,
         }
         print(json.dumps(out), flush=True)

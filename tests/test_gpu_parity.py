@@ -185,3 +185,25 @@ def test_oracle_parity_random_actions(cfg):
         assert np.array_equal(env.n_act.cpu().numpy(), ref.n_act)
         assert np.array_equal(f, ref.flags), f"step {t}: flags"
         assert np.array_equal(env.eff.cpu().numpy().view(np.uint64), ref.eff), f"step {t}: eff"
+
+
+@pytest.mark.parametrize("R,C,k,sm", [(10, 10, 4, 0), (8, 8, 3, 15), (20, 20, 6, 15)])
+def test_env_groups_match_single_stream(R, C, k, sm):
+    """TileMatchVecEnv(groups=3) — env groups on separate HIP streams — equals groups=1 bit for bit."""
+    from tile_match_gym_amd.shard import synthetic_actions
+    from tile_match_gym_amd.vec_env import TileMatchVecEnv
+    cl = ["cookie"] if sm & 1 else []
+    co = [nm for b, nm in ((8, "bomb"), (2, "vertical_laser"), (4, "horizontal_laser")) if sm & b]
+    n = 1000
+    e1 = TileMatchVecEnv(n, R, C, k, 12, cl, co, seed=77, device=DEV)
+    e3 = TileMatchVecEnv(n, R, C, k, 12, cl, co, seed=77, device=DEV, groups=3)
+    acts = torch.from_numpy(synthetic_actions(range(n), 30, e1.num_actions)).to(DEV)
+    e1.reset()
+    e3.reset()
+    for t in range(30):
+        e1.step_raw(acts[t])
+        e3.step_raw(acts[t])
+    e3.join()
+    torch.cuda.synchronize()
+    for f in ("board", "rng", "timer", "eff", "reward", "n_new", "n_act", "flags"):
+        assert torch.equal(getattr(e1, f), getattr(e3, f)), f

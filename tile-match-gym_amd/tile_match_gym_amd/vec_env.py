@@ -10,6 +10,13 @@ Autoreset (default on): an env whose episode ends is regenerated inside the
 same step call, continuing its RNG stream (== the reference's reset() without
 a seed, tile_match_env.py:84-87); reward/flags describe the final move,
 `info["final_board"]` is not kept (pass autoreset=False to inspect it).
+
+groups > 1: the envs are split into that many contiguous groups, each stepped
+on its own HIP stream, so the tail of one group's launch overlaps the next
+launch of another (envs are independent; results are identical to
+groups=1).  `step_raw` then only enqueues: call `join()` before reading the
+state or outputs on the current stream (`step`, `reset` and the other
+accessors join themselves).
 """
 from __future__ import annotations
 
@@ -51,7 +58,7 @@ def _ptr(t: torch.Tensor):
 class TileMatchVecEnv:
     def __init__(self, num_envs: int, num_rows: int, num_cols: int, num_colours: int, num_moves: int,
                  colourless_specials=(), colour_specials=(), seed: int = 0, seeds=None, device=None,
-                 autoreset: bool = True):
+                 autoreset: bool = True, groups: int = 1):
         if device is None:
             device = torch.device("cuda", torch.cuda.current_device())
         device = torch.device(device)
@@ -81,6 +88,19 @@ class TileMatchVecEnv:
         self.n_act = torch.zeros(N, dtype=torch.int32, **kw)
         self.flags = torch.zeros(N, dtype=torch.uint8, **kw)
         self._eff_valid = False
+        groups = max(1, min(int(groups), N))
+        self.groups = groups
+        bounds = [g * N // groups for g in range(groups + 1)]
+        self._ranges = [(bounds[g], bounds[g + 1]) for g in range(groups) if bounds[g + 1] > bounds[g]]
+        self._streams = [torch.cuda.Stream(device) for _ in self._ranges] if groups > 1 else []
+        self._ev_in = torch.cuda.Event() if groups > 1 else None
+        self._ev_out = [torch.cuda.Event() for _ in self._streams]
+        W, plane = self.mask_words, 2 * num_rows * num_cols
+        # per group: (n, board, rng, timer, eff, reward, n_new, n_act, flags) pointers
+        self._gptr = [(hi - lo, self.board.data_ptr() + lo * plane, self.rng.data_ptr() + lo * 40,
+                       self.timer.data_ptr() + lo * 4, self.eff.data_ptr() + lo * 8 * W,
+                       self.reward.data_ptr() + lo * 4, self.n_new.data_ptr() + lo * 4,
+                       self.n_act.data_ptr() + lo * 4, self.flags.data_ptr() + lo) for lo, hi in self._ranges]
 
     # ----------------------------------------------------------------- API
     def _stream(self):
@@ -91,7 +111,26 @@ class TileMatchVecEnv:
         w = batch_rng_words(seeds)
         self.rng.copy_(torch.from_numpy(w.view(np.int64)))
 
+    def _fork(self):
+        """Group streams wait for the work already queued on the current stream."""
+        self._ev_in.record(torch.cuda.current_stream(self.device))
+        for st in self._streams:
+            st.wait_event(self._ev_in)
+
+    def record(self, event, group: int = 0):
+        """Record `event` on the stream group `group` is stepped on (the current
+        stream for groups=1): HIP-event timing of that group's launches."""
+        event.record(self._streams[group] if self._streams else torch.cuda.current_stream(self.device))
+
+    def join(self):
+        """Make the current stream wait for every group's queued steps (no-op for groups=1)."""
+        cur = torch.cuda.current_stream(self.device)
+        for st, ev in zip(self._streams, self._ev_out):
+            ev.record(st)
+            cur.wait_event(ev)
+
     def reset(self, seed=None, env_mask=None):
+        self.join()
         if seed is not None:
             self.set_seed(range(int(seed), int(seed) + self.num_envs))
         m = None
@@ -110,6 +149,7 @@ class TileMatchVecEnv:
         if a.shape != (self.num_envs,):
             raise ValueError(f"actions must have shape ({self.num_envs},)")
         self.step_raw(a)
+        self.join()
         flags = self.flags
         info = {
             "is_combination_match": (flags & _native.FLAG_COMBO) != 0,
@@ -123,10 +163,21 @@ class TileMatchVecEnv:
         return self._obs(), self.reward, done, torch.zeros_like(done), info
 
     def step_raw(self, actions_i32: torch.Tensor):
-        """Enqueue one batched step (no output post-processing): the bench path."""
-        self.ctx.step(self.num_envs, _ptr(self.board), _ptr(self.rng), _ptr(self.timer), _ptr(actions_i32),
-                      _ptr(self.reward), _ptr(self.n_new), _ptr(self.n_act), _ptr(self.flags), _ptr(self.eff),
-                      int(self._eff_valid), int(self.autoreset), self._stream())
+        """Enqueue one batched step (no output post-processing): the bench path.
+        actions_i32: contiguous int32 (N,) on the device.  With groups > 1 call
+        join() before reading results."""
+        trust, auto = int(self._eff_valid), int(self.autoreset)
+        if not self._streams:
+            self.ctx.step(self.num_envs, _ptr(self.board), _ptr(self.rng), _ptr(self.timer), _ptr(actions_i32),
+                          _ptr(self.reward), _ptr(self.n_new), _ptr(self.n_act), _ptr(self.flags), _ptr(self.eff),
+                          trust, auto, self._stream())
+        else:
+            self._fork()
+            a0 = actions_i32.data_ptr()
+            for (lo, _), st, p in zip(self._ranges, self._streams, self._gptr):
+                actions_i32.record_stream(st)
+                self.ctx.step(p[0], p[1], p[2], p[3], a0 + 4 * lo, p[5], p[6], p[7], p[8], p[4], trust, auto,
+                              st.cuda_stream)
         self._eff_valid = True
 
     def invalidate_effective_cache(self):
@@ -134,6 +185,7 @@ class TileMatchVecEnv:
         self._eff_valid = False
 
     def compute_effective(self):
+        self.join()
         self.ctx.effective(self.num_envs, _ptr(self.board), _ptr(self.eff), self._stream())
         return self.eff
 
@@ -147,6 +199,7 @@ class TileMatchVecEnv:
         return {"board": self.board, "num_moves_left": self.num_moves - self.timer}
 
     def rng_words(self) -> np.ndarray:
+        self.join()
         return self.rng.cpu().numpy().view(np.uint64)
 
     # ------------------------------------------------------- checkpoint/restore
@@ -160,6 +213,7 @@ class TileMatchVecEnv:
         position of every env (incl. numpy's buffered half-word), timers and the
         effective-action masks; restoring it continues every trajectory
         bit-exactly."""
+        self.join()
         torch.cuda.synchronize(self.device)
         return {"board": self.board.cpu().numpy(), "rng": self.rng_words().copy(),
                 "timer": self.timer.cpu().numpy(), "eff": self.eff.cpu().numpy().view(np.uint64).copy(),
