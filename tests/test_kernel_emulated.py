@@ -81,3 +81,28 @@ def test_random_rollouts_emulated(emu_lib, cfg):
             o.step(a, True)
         for f in ("board", "rng", "eff", "reward", "flags", "timer", "n_new", "n_act"):
             assert np.array_equal(getattr(e, f), getattr(o, f)), f"{cfg} step {t}: {f}"
+
+
+def test_move_golden_emulated(emu_lib):
+    """Board.move (board.py:330-395) from the recorded arbitrary boards (specials, coloured cookies,
+    empties), through the emulated general kernel — the CPU twin of test_move_golden_gpu."""
+    from golden_io import load_records
+    emu, L = emu_lib
+    groups = {}
+    for r in load_records("move"):
+        if not r["err"]:
+            groups.setdefault((r["R"], r["C"], r["k"], r["smask"]), []).append(r)
+    total = 0
+    for (R, C, k, sm), recs in groups.items():
+        n = len(recs)
+        b = emu.EmuBatch(L, R, C, k, sm, 30, np.stack([r["rng_in"] for r in recs]).astype(np.uint64))
+        b.board[:] = np.stack([r["board"] for r in recs]).astype(np.int8)
+        b.trust = False
+        b.step(np.array([int(r["action"]) for r in recs], np.int32), autoreset=False)
+        for i, r in enumerate(recs):
+            res = r["res"]
+            assert np.array_equal(b.board[i], r["out"]), f"board {(R, C, k, sm)} rec {i}"
+            assert np.array_equal(b.rng[i], r["rng_out"]), f"rng {(R, C, k, sm)} rec {i}"
+            assert (b.reward[i], b.n_new[i], b.n_act[i]) == (res[0], res[2], res[3]), f"counters {(R, C, k, sm)} rec {i}"
+        total += n
+    assert total > 500

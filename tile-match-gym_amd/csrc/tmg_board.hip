@@ -1206,11 +1206,13 @@ struct Serial {
 };
 
 
+#include "tmg_sb.hip"
+
 // ------------------------------------------------------------------ move()
 // Board.move, board.py:330-395 (the effectiveness test :352 is done by the
 // caller).  Returns eliminations; leaves the effective mask of the final
 // board in w.effw.
-template <int MAXN, bool GEN>
+template <int MAXN, bool GEN, int SBNB, bool CODD>
 __device__ __forceinline__ int board_move(const Params &P, Ws<MAXN, GEN> &w, int lane, const LaneJump &J, Rng &g,
                           const Cells<MAXN / 64> &cl, int p1, int p2, int &flags, int &nn, int &na, int64_t e) {
     const int N = P.N;
@@ -1255,6 +1257,13 @@ __device__ __forceinline__ int board_move(const Params &P, Ws<MAXN, GEN> &w, int
     (void)e;
     while (!ovf && !err) {                                                  // :367-376
         if (w.sc[SC_ERR]) break;
+        if constexpr (GEN && SBNB > 0) {
+            if (!fast) {                    // bitboard step when it provably creates / activates no special
+                const int r = sb_simple_step<SBNB, CODD>(P, w, lane, J, g);
+                if (r < 0) break;
+                if (r > 0) { elim += r; iters++; continue; }
+            }
+        }
         Det<MAXN / 64> d;
         const int rs = detect(P, w, lane, cl, d);
         if (rs < 0) break;
@@ -1293,8 +1302,6 @@ __device__ __forceinline__ int board_move(const Params &P, Ws<MAXN, GEN> &w, int
     STAMP(e, 3);
     return elim;
 }
-
-#include "tmg_sb.hip"
 
 // ------------------------------------------------------------------ kernels
 __device__ __forceinline__ LaneJump load_jump(const Params &P, int lane, const Rng &g) {
@@ -1379,7 +1386,7 @@ __device__ __forceinline__ void step_env(
     STAMP(e, 1);
     if (effective) {
         if constexpr (SBNB > 0 && !GEN) elim = sb_move<SBNB, CODD>(P, w, lane, J, g, cl, p1, p2, flags, e);
-        else elim = board_move(P, w, lane, J, g, cl, p1, p2, flags, nn, na, e);
+        else elim = board_move<MAXN, GEN, SBNB, CODD>(P, w, lane, J, g, cl, p1, p2, flags, nn, na, e);
         changed = true;
     }
     STAMP(e, 4);

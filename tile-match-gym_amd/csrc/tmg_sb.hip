@@ -97,12 +97,14 @@ struct SBDet {
     Pair va, ha, neU, neR;
 };
 
+// z: colourless cells (cookies, colour 0), which match nothing (anchors need
+// type > 0, runs extend by colour, board.py:163-188, 196).
 template <int NB, bool CODD>
-__device__ __forceinline__ SBDet sb_detect(const Params &P, const SB<NB> &s) {
+__device__ __forceinline__ SBDet sb_detect(const Params &P, const SB<NB> &s, Pair z = Pair{0, 0}) {
     const int C = P.C;
     SBDet d;
-    d.neU = Pair{0, 0};
-    d.neR = Pair{0, 0};
+    d.neU = z | fwd<CODD>(z, C);
+    d.neR = z | bwd<true>(z, 1);
 #pragma unroll
     for (int b = 0; b < NB; b++) {
         d.neU = d.neU | (s.p[b] ^ fwd<CODD>(s.p[b], C));
@@ -154,34 +156,41 @@ __device__ __forceinline__ void sb_line_keys(const Params &P, int lane, int &key
     keyB = q1 < P.N ? ((r1 << 8) | (255 - (q1 - r1 * P.C))) << 1 : -1;
 }
 
-// One cascade step when no special can exist (board.py:367-376 with every
-// line a normal match): the union of get_colour_lines' lines in row rs —
-// first-pass lines (coords K) plus the perpendicular pass, which from every
-// coord walks each axis over non-coord cells of the same colour and keeps
-// runs of >= 3 (:195-214).
-template <int NB, bool CODD>
-__device__ __forceinline__ Pair sb_clear(const Params &P, const SBDet &d, int rs) {
+// The first-pass coords of get_colour_lines' bottom row rs (board.py:158-193):
+// kh = cells of its horizontal runs, kv = cells of the vertical runs ending
+// in it (from the bottom up while the colour holds, :166-172).
+template <bool CODD>
+__device__ __forceinline__ void sb_coords(const Params &P, const SBDet &d, int rs, Pair &kh, Pair &kv) {
     const int C = P.C;
-    const Pair inb{P.sb_in[0], P.sb_in[1]};
     const Pair row = sb_row(P, rs);
-    const Pair nf{P.sb_nf[0], P.sb_nf[1]};
-    const Pair eqR = andn(Pair{P.sb_nl[0], P.sb_nl[1]}, d.neR);   // same colour as the right neighbour
     const Pair eqU = andn(Pair{P.sb_u[0], P.sb_u[1]}, d.neU);      // same colour as the cell above
-    // first-pass coords: horizontal runs of row rs, vertical runs ending in it
     const Pair h = d.ha & row;
-    Pair K = h | fwd<true>(h, 1) | fwd<false>(h, 2);
+    kh = h | fwd<true>(h, 1) | fwd<false>(h, 2);
     const Pair v = d.va & row;
+    kv = Pair{0, 0};
     if (nonzero(v)) {
         Pair t = bwd<false>(v, 2 * C);
-        K = K | v | bwd<CODD>(v, C) | t;
+        kv = v | bwd<CODD>(v, C) | t;
         for (;;) {
             t = bwd<CODD>(t & eqU, C);
             if (!nonzero(t)) break;
-            K = K | t;
+            kv = kv | t;
         }
     }
-    Pair clr = K;
+}
+
+// get_colour_lines' perpendicular pass (board.py:195-214): from every coord of K
+// walk each axis over non-coord cells of the same colour; a run of >= 3 is a
+// line.  Adds the cells of those lines to clr; returns whether there is one.
+template <bool CODD>
+__device__ __forceinline__ bool sb_perpendicular(const Params &P, const SBDet &d, const Pair K, Pair &clr) {
+    const int C = P.C;
+    const Pair inb{P.sb_in[0], P.sb_in[1]};
+    const Pair nf{P.sb_nf[0], P.sb_nf[1]};
+    const Pair eqR = andn(Pair{P.sb_nl[0], P.sb_nl[1]}, d.neR);   // same colour as the right neighbour
+    const Pair eqU = andn(Pair{P.sb_u[0], P.sb_u[1]}, d.neU);      // same colour as the cell above
     const Pair walk = andn(inb, K);
+    bool any = false;
     // horizontal runs through coords
     const Pair r1 = fwd<true>(K & eqR, 1) & walk;
     const Pair l1 = bwd<true>(K & nf, 1) & eqR & walk;
@@ -190,6 +199,7 @@ __device__ __forceinline__ Pair sb_clear(const Params &P, const SBDet &d, int rs
         const Pair l2 = bwd<true>(l1 & nf, 1) & eqR & walk;
         const Pair q = K & (bwd<false>(r2, 2) | fwd<false>(l2, 2) | (bwd<true>(r1, 1) & fwd<true>(l1, 1)));
         if (nonzero(q)) {
+            any = true;
             Pair f = fwd<true>(q & eqR, 1) & walk;
             while (nonzero(f)) { clr = clr | f; f = fwd<true>(f & eqR, 1) & walk; }
             Pair g = bwd<true>(q & nf, 1) & eqR & walk;
@@ -204,12 +214,25 @@ __device__ __forceinline__ Pair sb_clear(const Params &P, const SBDet &d, int rs
         const Pair u2 = bwd<CODD>(u1 & eqU, C) & walk;
         const Pair q = K & (fwd<false>(u2, 2 * C) | bwd<false>(d2, 2 * C) | (fwd<CODD>(u1, C) & bwd<CODD>(d1, C)));
         if (nonzero(q)) {
+            any = true;
             Pair f = fwd<CODD>(q, C) & eqU & walk;
             while (nonzero(f)) { clr = clr | f; f = fwd<CODD>(f, C) & eqU & walk; }
             Pair g = bwd<CODD>(q & eqU, C) & walk;
             while (nonzero(g)) { clr = clr | g; g = bwd<CODD>(g & eqU, C) & walk; }
         }
     }
+    return any;
+}
+
+// One cascade step when no special can exist (board.py:367-376 with every
+// line a normal match): the union of get_colour_lines' lines in row rs.
+template <int NB, bool CODD>
+__device__ __forceinline__ Pair sb_clear(const Params &P, const SBDet &d, int rs) {
+    Pair kh, kv;
+    sb_coords<CODD>(P, d, rs, kh, kv);
+    const Pair K = kh | kv;
+    Pair clr = K;
+    sb_perpendicular<CODD>(P, d, K, clr);
     return clr;
 }
 
@@ -218,11 +241,13 @@ __device__ __forceinline__ Pair sb_clear(const Params &P, const SBDet &d, int rs
 // drops by the empties below it in its column, the top `empties` cells of a
 // column take the refill draws in row-major order.  Leaves the new board in
 // LDS and in c.
-template <bool CODD, class WS>
+// TYPES: move the type plane too (boards with specials); the refilled cells
+// become normal tiles (type 1).  Without it the type plane is all 1 and stays.
+template <bool CODD, bool TYPES = false, class WS>
 __device__ __forceinline__ void sb_gravity_refill(const Params &P, WS &w, int lane, const LaneJump &J, Rng &g,
                                                   const Pair E, int total, SBC &c) {
     const int N = P.N, C = P.C;
-    int8_t *col = w.brd;
+    int8_t *col = w.brd, *typ = w.brd + N;
     const int q0 = 2 * lane, q1 = q0 + 1;
     const int r0 = div_c(P, q0), c0 = q0 - r0 * C;
     const int r1 = div_c(P, q1), c1 = q1 - r1 * C;
@@ -252,6 +277,11 @@ __device__ __forceinline__ void sb_gravity_refill(const Params &P, WS &w, int la
     const uint64_t lt = lanemask_lt(lane);
     const int rank0 = __popcll(NA & lt) + __popcll(NBm & lt);
     const int rank1 = rank0 + (n0 ? 1 : 0);
+    int8_t y0 = 1, y1 = 1;
+    if constexpr (TYPES) {
+        y0 = typ[v0 ? q0 : 0];
+        y1 = typ[v1 ? q1 : 0];
+    }
     draw_colours(P, lane, J, g, total, w.u.draw, w.trash);
     WSYNC();
     const int8_t d0 = (int8_t)w.u.draw[n0 ? rank0 : 0], d1 = (int8_t)w.u.draw[n1 ? rank1 : 0];
@@ -260,6 +290,13 @@ __device__ __forceinline__ void sb_gravity_refill(const Params &P, WS &w, int la
     *(v1 && !e1 ? col + q1 + below1 * C : w.trash + 64 + lane) = (int8_t)(c.b + 1);
     *(n0 ? col + q0 : w.trash + 128 + lane) = d0;
     *(n1 ? col + q1 : w.trash + 192 + lane) = d1;
+    if constexpr (TYPES) {
+        WFENCE();
+        *(v0 && !e0 ? typ + q0 + below0 * C : w.trash + lane) = y0;
+        *(v1 && !e1 ? typ + q1 + below1 * C : w.trash + 64 + lane) = y1;
+        *(n0 ? typ + q0 : w.trash + 128 + lane) = (int8_t)1;
+        *(n1 ? typ + q1 : w.trash + 192 + lane) = (int8_t)1;
+    }
     WSYNC();
     c = sb_codes_from_lds(P, col, lane);
 }
@@ -387,4 +424,59 @@ __device__ __forceinline__ int sb_move(const Params &P, WS &w, int lane, const L
     if (sb_ensure<NB, CODD>(P, w, lane, J, g, cl, c, false, true)) flags |= FL_SHUF;   // :381-391
     STAMP(e, 3);
     return elim;
+}
+
+// One cascade step of the general kernel (specials enabled, board.py:367-376)
+// on bitboards, when it provably reduces to the no-specials union clear:
+// get_colour_lines yields no perpendicular line, process_colour_lines
+// (:269-327) turns every first-pass line into a normal match — no 4-line when
+// a laser is enabled (a horizontal one only counts for the h-laser or the
+// v-laser, a vertical one for the v-laser, :294-302), no 5+-line when cookies
+// are, no two lines sharing a cell when bombs are (:304-320) — and no cleared
+// cell holds a special to activate (resolve_colour_match, :460-471).
+// Returns -1 when there is no line, 0 when the step is not of that kind (the
+// caller runs the list machinery on the unchanged LDS board), otherwise the
+// number of cleared cells (the board in LDS has been cleared, dropped and
+// refilled).
+template <int NB, bool CODD, class WS>
+__device__ __forceinline__ int sb_simple_step(const Params &P, WS &w, int lane, const LaneJump &J, Rng &g) {
+    const int N = P.N, C = P.C;
+    const int8_t *col = w.brd, *typ = w.brd + N;
+    const int q0 = 2 * lane;
+    const int x0 = q0 < N ? (int)col[q0] : 1, x1 = q0 + 1 < N ? (int)col[q0 + 1] : 1;
+    const int y0 = q0 < N ? (int)typ[q0] : 1, y1 = q0 + 1 < N ? (int)typ[q0 + 1] : 1;
+    // the bitboards model tiles of type >= 1 with colours 1..k and colourless
+    // cookies; empty cells (gravity would move them too), cookies that gained a
+    // colour (remove_colour_lines, :129) and out-of-range values take the list path
+    const auto odd_cell = [&](int x, int y) { return y == 0 || (y < 0 && x != 0) || x < 0 || x > P.k; };
+    if (__ballot(odd_cell(x0, y0) || odd_cell(x1, y1)) != 0ULL) return 0;
+    SBC c{x0 - 1, x1 - 1};
+    const Pair z{__ballot(x0 == 0), __ballot(x1 == 0)};                    // colourless (cookies)
+    const SBDet d = sb_detect<NB, CODD>(P, sb_planes_of<NB>(c), z);
+    const int rs = sb_bottom_row(P, d);
+    if (rs < 0) return -1;
+    const int S = P.smask;
+    const Pair row = sb_row(P, rs);
+    const Pair eqU = andn(Pair{P.sb_u[0], P.sb_u[1]}, d.neU);
+    // first-pass line lengths: a horizontal run of L cells holds L-2 anchors
+    const Pair h = d.ha & row;
+    const Pair h2 = h & bwd<true>(h, 1);
+    const bool h4 = nonzero(andn(andn(h2, bwd<false>(h, 2)), fwd<true>(h, 1)));
+    const bool h5 = nonzero(h2 & bwd<false>(h, 2));
+    const Pair x4 = bwd<CODD>(bwd<false>(d.va & row, 2 * C) & eqU, C);    // 4th cell of a vertical run
+    const bool v4 = nonzero(andn(x4, eqU)), v5 = nonzero(x4 & eqU);
+    if (h4 && (S & (SP_HLASER | SP_VLASER))) return 0;
+    if (v4 && (S & SP_VLASER)) return 0;
+    if ((h5 || v5) && (S & SP_COOKIE)) return 0;
+    Pair kh, kv;
+    sb_coords<CODD>(P, d, rs, kh, kv);
+    if ((S & SP_BOMB) && nonzero(kh & kv)) return 0;
+    const Pair K = kh | kv;
+    const Pair sp{__ballot(y0 >= 2), __ballot(y1 >= 2)};                  // lasers / bombs
+    if (nonzero(K & sp)) return 0;
+    Pair clr = K;
+    if (sb_perpendicular<CODD>(P, d, K, clr)) return 0;
+    const int tot = popc(clr);
+    sb_gravity_refill<CODD, true>(P, w, lane, J, g, clr, tot, c);
+    return tot;
 }
