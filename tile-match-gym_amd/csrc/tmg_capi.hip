@@ -33,6 +33,7 @@ struct tmg_ctx {
     uint64_t *d_sbrows;
     int maxn;
     int sb;          // scalar-bitboard kernels usable (<= 128 cells, C <= 63); TMG_SB=0 disables (A/B)
+    int defer_general;   // 128-cell general kernel: autoreset by a masked reset launch (TMG_DEFER=0 disables)
 };
 
 using tmg::Params;
@@ -121,7 +122,7 @@ static int do_step(tmg_ctx *ctx, StepArgs a, hipStream_t s) {
     const bool lean = P.smask == 0 && a.trust_eff;
     const dim3 grid = env_grid(a.n);
     a.autoreset = a.autoreset ? 1 : 0;
-    if (ctx->maxn == 128) {
+    if (ctx->maxn == 128 && !(ctx->defer_general && !lean && a.autoreset)) {
         if (ctx->sb) {
             if (lean) {
                 if (P.C & 1) launch_step_sb<false, true>(grid, s, P, a);
@@ -137,12 +138,19 @@ static int do_step(tmg_ctx *ctx, StepArgs a, hipStream_t s) {
         }
         return hip_check(hipGetLastError(), "kernel launch");
     }
-    // 512-cell kernels: finished boards are regenerated by a reset_kernel launch
-    // masked by FL_RESET, which runs at several times the step kernel's occupancy
+    // 512-cell kernels (and, with defer_general, the 128-cell general one):
+    // finished boards are regenerated by a reset_kernel launch masked by
+    // FL_RESET, which runs at several times the step kernel's occupancy
     const int deferred = a.autoreset;
     if (deferred) a.autoreset = 2;
-    if (lean) launch_step<512, false, 0, false>(grid, s, P, a);
-    else launch_step<512, true, 0, false>(grid, s, P, a);
+    if (ctx->maxn == 128) {
+        if (P.C & 1) launch_step_sb<true, true>(grid, s, P, a);
+        else launch_step_sb<true, false>(grid, s, P, a);
+    } else if (lean) {
+        launch_step<512, false, 0, false>(grid, s, P, a);
+    } else {
+        launch_step<512, true, 0, false>(grid, s, P, a);
+    }
     int rc = hip_check(hipGetLastError(), "kernel launch");
     if (rc || !deferred) return rc;
     return do_reset(ctx, a.n, a.board, a.rng, a.timer, a.eff, a.flags, tmg::FL_RESET, s);
@@ -185,8 +193,10 @@ int tmg_create(tmg_ctx **out, int device, int rows, int cols, int colours, uint3
     c->P = tmg::make_params(rows, cols, colours, (int)specials_mask, num_moves, nullptr);
     Params &P = c->P;
     c->maxn = P.N <= 128 ? 128 : 512;
+    const char *denv = getenv("TMG_DEFER");
     const char *sbenv = getenv("TMG_SB");
     c->sb = P.N <= 128 && P.C <= 63 && !(sbenv && sbenv[0] == '0');
+    c->defer_general = c->sb && !(denv && denv[0] == '0');
     uint64_t tab[64 * 4];
     tmg::build_jump_table(tab);
     rc = hip_check(hipMalloc(&c->d_jump, sizeof tab), "hipMalloc");

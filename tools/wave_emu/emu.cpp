@@ -288,7 +288,13 @@ int emu_step(int R, int C, int k, int smask, int moves, int64_t n, int8_t *board
     if (P.N <= 128) {
         if (sb_ok(P)) {
             if (lean) { if (P.C & 1) emu_step_sb<false, true>(S); else emu_step_sb<false, false>(S); }
-            else { if (P.C & 1) emu_step_sb<true, true>(S); else emu_step_sb<true, false>(S); }
+            else {
+                // general kernel: autoreset deferred to a FL_RESET-masked reset, as tmg_capi.hip
+                const int deferred = S.autoreset;
+                if (deferred) S.autoreset = 2;
+                if (P.C & 1) emu_step_sb<true, true>(S); else emu_step_sb<true, false>(S);
+                if (deferred) emu_do_reset(P, n, board, rng, timer, eff, flags, tmg::FL_RESET);
+            }
         } else if (lean) {
             emu_step_kernel<128, false, 0, false>(S);
         } else {
