@@ -47,6 +47,10 @@ namespace tmg {
 #define TMG_XCD 1          // XCD-aware workgroup -> env mapping
 #endif
 
+#ifndef TMG_RESET512_WAVES
+#define TMG_RESET512_WAVES 4   // min waves per SIMD for the 512-cell reset kernel (caps its VGPRs)
+#endif
+
 // compiler-only ordering point between a wave's LDS loads and later stores
 #define WFENCE() __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront")
 
@@ -177,14 +181,19 @@ struct WsCore {
     } u;
 };
 
+// Capacities of the lane-0 lists.  A cascade step of a real board uses a few
+// dozen entries; the 512-cell workspace is sized at half the cell count so
+// the general 20x20 kernel fits twice the waves per CU in LDS.  Running out
+// sets FL_OVF (the step is then not trusted) rather than corrupting memory.
 template <int MAXN>
 struct WsSerial {                                   // lane-0 list machinery (general variant only)
-    static constexpr int POOL = 4 * MAXN + 256;     // coords of lines
-    static constexpr int MLINES = MAXN + 64;        // lines
-    static constexpr int MQ = 2 * MAXN + 64;        // process queue
-    static constexpr int MM = MAXN + 32;            // matches
-    static constexpr int MPOOL = 4 * MAXN + 256;    // coords of matches
-    static constexpr int MSTK = MAXN + 8;           // activation DFS frames
+    static constexpr int CAP = MAXN > 128 ? MAXN / 2 : MAXN;
+    static constexpr int POOL = 4 * CAP + 256;      // coords of lines
+    static constexpr int MLINES = CAP + 64;         // lines
+    static constexpr int MQ = 2 * CAP + 64;         // process queue
+    static constexpr int MM = CAP + 32;             // matches
+    static constexpr int MPOOL = 4 * CAP + 256;     // coords of matches
+    static constexpr int MSTK = CAP + 8;            // activation DFS frames
     static constexpr int MV = 96;                   // coords of one match
     int16_t pool[POOL];
     int16_t ls[MLINES], ll[MLINES];
@@ -1444,7 +1453,7 @@ __global__ TMG_LAUNCH_BOUNDS void step_kernel(
 
 // TileMatchEnv.reset without a seed (tile_match_env.py:84-91)
 template <int MAXN, int SBNB = 0, bool CODD = false>
-__global__ TMG_LAUNCH_BOUNDS void reset_kernel(Params P, int64_t n, int8_t *__restrict__ board,
+__global__ __launch_bounds__(64 * TMG_WPB, MAXN > 128 ? TMG_RESET512_WAVES : 1) void reset_kernel(Params P, int64_t n, int8_t *__restrict__ board,
                                                              uint64_t *__restrict__ rng, int32_t *__restrict__ timer,
                                                              uint64_t *__restrict__ eff,
                                                              const uint8_t *__restrict__ env_mask, int mask_bits) {
