@@ -172,6 +172,10 @@ struct WsCore {
     static constexpr int MAXW = (2 * MAXN) / 64 + 2;
     uint64_t effw[MAXW];
     int32_t sc[SC_COUNT];
+    // brd sits >= 128 bytes into the workspace, so the effective-action scan's
+    // neighbour reads at p - 2C (C <= 64) stay inside it without clamping
+    static constexpr int PRE = MAXW * 8 + SC_COUNT * 4;
+    int8_t lpad[PRE >= 128 ? 1 : 128 - PRE];
     int8_t brd[2 * MAXN];          // [colour plane N][type plane N], runtime N (same layout as HBM)
     uint8_t mark[MAXN];
     alignas(8) int8_t trash[4 * 64];   // target of predicated-off stores (keeps hot loops branch-free)
@@ -357,18 +361,6 @@ __device__ __forceinline__ void action_coords(int R, int C, int a, int &r1, int 
     if (a < C * (R - 1)) { r1 = a / C; c1 = a % C; r2 = r1 + 1; c2 = c1; }
     else { int i = a - C * (R - 1); r1 = i / (C - 1); c1 = i % (C - 1); r2 = r1; c2 = c1 + 1; }
 }
-// same, branch-free, for lane-parallel scans (a < 2^10)
-__device__ __forceinline__ void action_coords_fast(const Params &P, int a, int &r1, int &c1, int &r2, int &c2) {
-    const int C = P.C, nv = C * (P.R - 1);
-    const bool vert = a < nv;
-    const int i = vert ? a : a - nv;
-    const int q = vert ? div_c(P, i) : div_cm1(P, i);
-    r1 = q;
-    c1 = i - q * (vert ? C : C - 1);
-    r2 = r1 + (vert ? 1 : 0);
-    c2 = c1 + (vert ? 0 : 1);
-}
-
 // per-lane cell coordinates of each 64-cell pass, computed once per kernel
 template <int NP>
 struct Cells {
@@ -446,39 +438,76 @@ __device__ __forceinline__ bool eff_exact(const Params &P, const int8_t *brd, in
     return false;
 }
 
-// Same predicate when the board holds no cookie and no pre-existing colour
-// triple (checked by the caller): only triples through exactly one of the two
-// swapped cells can appear, all inside the reference's window.  Branch-free:
-// out-of-board neighbours read a clamped cell and are masked to a sentinel.
-__device__ __forceinline__ uint32_t eff_fast(const Params &P, const int8_t *brd, int a) {   // 0 iff effective
+// is_move_effective for every action of a clean board (no cookie, no
+// pre-existing colour triple, checked by the caller): only triples through
+// exactly one of the two swapped cells can appear, all inside the window.  Pass i
+// takes vertical action i and horizontal action nv + i on every lane; within
+// a direction each swapped pair's 14 neighbours sit at the same offsets (±1,
+// ±2, ±C, ±2C), so each is an LDS byte read at a uniform offset (WsCore::lpad
+// keeps the negative ones inside the workspace) and a validity term.
+// Swapping p (top / left) with q: p takes q's colour x2, q takes x1, and
+// either needs a triple away from the other cell or across its own axis
+// (tile_match_env.py:118-124, board.py:735-787).  Predicates are "zero means
+// true" integers (VALU, no lane-mask SALU).  TYPES = false: every type is 1.
+// Fills w.effw.
+template <bool TYPES, class WS>
+__device__ __forceinline__ bool scan_effective_clean(const Params &P, WS &w, int lane) {
     const int R = P.R, C = P.C, N = P.N;
-    int r1, c1, r2, c2;
-    action_coords_fast(P, a, r1, c1, r2, c2);
-    const int8_t *col = brd, *typ = brd + N;
-    const int p = r1 * C + c1, q = r2 * C + c2;
-    const uint32_t tp = (uint32_t)(int)typ[p], tq = (uint32_t)(int)typ[q];
-    const uint32_t not_both_special = umin(tp, tq) > 1u ? 0u : 1u;    // type not in {0,1} (no cookies here)
-    const int x1 = col[p], x2 = col[q];
-    auto at = [&](int r, int c) -> int {        // colour, or -64 outside the board
-        const int oob = r | (R - 1 - r) | c | (C - 1 - c);     // negative iff outside
-        const int v = col[max(min(r, R - 1), 0) * C + max(min(c, C - 1), 0)];
-        return oob < 0 ? -64 : v;
+    const int8_t *col = w.brd, *typ = w.brd + N;
+    const int nv = C * (R - 1), nh = R * (C - 1);            // board.py:77-93
+    if (lane < P.W) w.effw[lane] = 0ULL;
+    WFENCE();
+    const auto neg = [](int v) -> uint32_t { return (uint32_t)(v >> 31); };               // ~0 iff v < 0
+    const auto nq = [](int a, int b, uint32_t inv) -> uint32_t { return (uint32_t)(a ^ b) | inv; };
+    const auto place = [&](uint64_t m, int at) {             // lane 0: OR ballot m into bits [at, at + 64)
+        const int wi = at >> 6, sh = at & 63;
+        w.effw[wi] |= m << sh;
+        const uint64_t hi = sh ? m >> (64 - sh) : 0ULL;
+        if (hi) w.effw[wi + 1] |= hi;
     };
-    const bool vert = r2 == r1 + 1;
-    const int dr = vert ? 1 : 0, dc = 1 - dr;                 // unit step along the pair
-    const int er = dc, ec = dr;                               // unit step across
-    // p receives x2 (neighbours on p's side), q receives x1 (q's side)
-    const int pa1 = at(r1 - dr, c1 - dc), pa2 = at(r1 - 2 * dr, c1 - 2 * dc);
-    const int qa1 = at(r2 + dr, c2 + dc), qa2 = at(r2 + 2 * dr, c2 + 2 * dc);
-    const int pm1 = at(r1 - er, c1 - ec), pm2 = at(r1 - 2 * er, c1 - 2 * ec);
-    const int pp1 = at(r1 + er, c1 + ec), pp2 = at(r1 + 2 * er, c1 + 2 * ec);
-    const int qm1 = at(r2 - er, c2 - ec), qm2 = at(r2 - 2 * er, c2 - 2 * ec);
-    const int qp1 = at(r2 + er, c2 + ec), qp2 = at(r2 + 2 * er, c2 + 2 * ec);
-    const uint32_t hp = umin3(ne(pa1, x2) | ne(pa2, x2), ne(pm1, x2) | umin(ne(pm2, x2), ne(pp1, x2)),
-                              ne(pp1, x2) | ne(pp2, x2));
-    const uint32_t hq = umin3(ne(qa1, x1) | ne(qa2, x1), ne(qm1, x1) | umin(ne(qm2, x1), ne(qp1, x1)),
-                              ne(qp1, x1) | ne(qp2, x1));
-    return umin3(not_both_special, hp, hq);
+    uint64_t any = 0;
+    for (int base = 0; base < (nv > nh ? nv : nh); base += 64) {
+        const int i = base + lane;
+        uint32_t fv, fh;                                     // 0 iff effective
+        {   // vertical action i: p = i (top cell), q = p + C
+            const int p = i < nv ? i : 0, q = p + C;
+            const int r = div_c(P, p), c = p - r * C;
+            const int x1 = col[p], x2 = col[q];
+            const uint32_t l1 = neg(c - 1), l2 = neg(c - 2), g1 = neg(C - 2 - c), g2 = neg(C - 3 - c);
+            const uint32_t hp = umin3(nq(col[p - C], x2, neg(r - 1)) | nq(col[p - 2 * C], x2, neg(r - 2)),
+                                      nq(col[p - 1], x2, l1) | umin(nq(col[p - 2], x2, l2), nq(col[p + 1], x2, g1)),
+                                      nq(col[p + 1], x2, g1) | nq(col[p + 2], x2, g2));
+            const uint32_t hq = umin3(nq(col[q + C], x1, neg(R - 3 - r)) | nq(col[q + 2 * C], x1, neg(R - 4 - r)),
+                                      nq(col[q - 1], x1, l1) | umin(nq(col[q - 2], x1, l2), nq(col[q + 1], x1, g1)),
+                                      nq(col[q + 1], x1, g1) | nq(col[q + 2], x1, g2));
+            uint32_t sp = 1u;                                // 0 iff both are specials (type not in {0, 1})
+            if constexpr (TYPES) sp = umin((uint32_t)(int)typ[p], (uint32_t)(int)typ[q]) > 1u ? 0u : 1u;
+            fv = umin3(sp, hp, hq) | neg(nv - 1 - i);
+        }
+        {   // horizontal action nv + i: i = r*(C-1) + c, p = r*C + c, q = p + 1
+            const int ih = i < nh ? i : 0;
+            const int r = div_cm1(P, ih), c = ih - r * (C - 1);
+            const int p = r * C + c, q = p + 1;
+            const int x1 = col[p], x2 = col[q];
+            const uint32_t u1 = neg(r - 1), u2 = neg(r - 2), d1 = neg(R - 2 - r), d2 = neg(R - 3 - r);
+            const uint32_t hp = umin3(nq(col[p - 1], x2, neg(c - 1)) | nq(col[p - 2], x2, neg(c - 2)),
+                                      nq(col[p - C], x2, u1) | umin(nq(col[p - 2 * C], x2, u2), nq(col[p + C], x2, d1)),
+                                      nq(col[p + C], x2, d1) | nq(col[p + 2 * C], x2, d2));
+            const uint32_t hq = umin3(nq(col[q + 1], x1, neg(C - 3 - c)) | nq(col[q + 2], x1, neg(C - 4 - c)),
+                                      nq(col[q - C], x1, u1) | umin(nq(col[q - 2 * C], x1, u2), nq(col[q + C], x1, d1)),
+                                      nq(col[q + C], x1, d1) | nq(col[q + 2 * C], x1, d2));
+            uint32_t sp = 1u;
+            if constexpr (TYPES) sp = umin((uint32_t)(int)typ[p], (uint32_t)(int)typ[q]) > 1u ? 0u : 1u;
+            fh = umin3(sp, hp, hq) | neg(nh - 1 - i);
+        }
+        const uint64_t mv = __ballot(fv == 0u), mh = __ballot(fh == 0u);
+        any |= mv | mh;
+        if (lane == 0) {
+            if (mv) place(mv, base);
+            if (mh) place(mh, nv + base);
+        }
+    }
+    return any != 0ULL;
 }
 
 // _get_effective_actions / possible_move (tile_match_env.py:118-124, board.py:558-569):
@@ -504,12 +533,11 @@ __device__ __forceinline__ bool scan_effective(const Params &P, WS &w, int lane,
         }
         exact = __ballot(odd) != 0ULL;
     }
+    if (!exact) return scan_effective_clean<true>(P, w, lane);
     uint64_t any = 0;
     for (int base = 0, wi = 0; base < P.A; base += 64, wi++) {
         int a = base + lane;
-        bool e = false;
-        if (exact) e = a < P.A && eff_exact(P, w.brd, a);
-        else e = (eff_fast(P, w.brd, min(a, P.A - 1)) | (a < P.A ? 0u : 1u)) == 0u;
+        const bool e = a < P.A && eff_exact(P, w.brd, a);
         uint64_t m = __ballot(e);
         if (lane == 0) w.effw[wi] = m;
         any |= m;

@@ -375,7 +375,7 @@ __device__ __forceinline__ bool sb_ensure(const Params &P, WS &w, int lane, cons
             WSYNC();
             dirty = false;
         }
-        if (scan_effective(P, w, lane, cl, true)) break;
+        if (scan_effective_clean<false>(P, w, lane)) break;   // types all 1, no line
         WSYNC();
         shuffle(P, w, lane, g);
         c = sb_codes_from_lds(P, w.brd, lane);
