@@ -48,10 +48,11 @@ def algorithmic_bytes_per_env_step(R, C):
     return 4 * R * C + 48 + 8 + 4 + 8 + 16 + 8 * ((A + 63) // 64)
 
 
-def cpu_baseline(R, C, k, smask, moves, budget_s=12.0):
+def cpu_baseline(R, C, k, smask, moves, budget_s=12.0, policy="uniform"):
     """The oracle (oracle/tmg_oracle.c, a bit-exact C port of the reference
     Board) timed on this host's cores over a bounded sample of the same
-    workload (same seeds / action distribution)."""
+    workload (same seeds / action distribution; for the effective-action policy
+    the numpy restatement of the sampler picks the actions, inside the timing)."""
     from oracle import oracle as orc
     from tile_match_gym_amd.seeding import batch_rng_words
     threads = min(16, os.cpu_count() or 1)
@@ -65,7 +66,12 @@ def cpu_baseline(R, C, k, smask, moves, budget_s=12.0):
     t0 = time.perf_counter()
     while True:
         for t in range(moves):
-            o.step(acts[(steps + t) % T], autoreset=True)
+            if policy == "effective":
+                from oracle.policy_np import sample_effective_np
+                a = sample_effective_np(o.eff, 2 * R * C - R - C, 12345, 0, steps + t)
+            else:
+                a = acts[(steps + t) % T]
+            o.step(a, autoreset=True)
         steps += moves
         el = time.perf_counter() - t0
         if el >= budget_s:
@@ -95,6 +101,9 @@ def main():
     ap.add_argument("--boards", type=int, default=0, help="override boards per GPU")
     ap.add_argument("--groups", type=int, default=3,
                     help="env groups per GPU, each stepped on its own HIP stream (TileMatchVecEnv(groups=))")
+    ap.add_argument("--policy", default="uniform", choices=("uniform", "effective"),
+                    help="uniform: random actions over all A (headline); effective: every env samples uniformly "
+                         "from its effective actions on device each step (SURVEY §8(d) secondary mode)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
 
@@ -122,8 +131,16 @@ def main():
     T = 300
     acts = torch.from_numpy(synthetic_actions(shard_range(rank, nb), T, A)).to(dev)
     env.reset()
+    first_env = shard_range(rank, nb).start
+
+    def step(t):
+        if args.policy == "effective":
+            env.step_effective(t, first_env=first_env)       # sampler + step, both on device
+        else:
+            env.step_raw(acts[t % T])
+
     for t in range(args.warmup):
-        env.step_raw(acts[t % T])
+        step(t)
     env.join()
     torch.cuda.synchronize()
 
@@ -137,7 +154,7 @@ def main():
     t0 = time.perf_counter()
     env.record(ev0)
     for i in range(args.steps):
-        env.step_raw(acts[(args.warmup + i) % T])
+        step(args.warmup + i)
     env.record(ev1)
     env.join()
     torch.cuda.synchronize()
@@ -158,7 +175,7 @@ def main():
         achieved = bpu * launch_envs / (kern_ms * 1e-3) / 1e9
         smask = (1 if "cookie" in cl else 0) | (2 if "vertical_laser" in co else 0) | \
                 (4 if "horizontal_laser" in co else 0) | (8 if "bomb" in co else 0)
-        cpu = None if (args.no_cpu_baseline or world > 1) else cpu_baseline(R, C, k, smask, moves)
+        cpu = None if (args.no_cpu_baseline or world > 1) else cpu_baseline(R, C, k, smask, moves, policy=args.policy)
         out = {
             "metric": METRIC,
             "value": round(value, 1),
@@ -171,8 +188,12 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "int8",
-            "data": "synthetic (uniform random actions, counter-based per (step, global env); seeds = global env index)",
-            "config": {"workload": f"{args.config}: {desc}, num_moves=30, autoreset",
+            "data": ("synthetic (uniform random actions, counter-based per (step, global env); seeds = global env index)"
+                     if args.policy == "uniform" else
+                     "synthetic (each step every env samples uniformly from its effective actions on device, "
+                     "counter-based per (step, global env); seeds = global env index)"),
+            "config": {"workload": f"{args.config}: {desc}, num_moves=30, autoreset"
+                                   + ("" if args.policy == "uniform" else ", effective-action policy"),
                        "boards_per_gpu": nb, "rows": R, "cols": C, "colours": k,
                        "specials": cl + co, "env_groups_per_gpu": env.groups,
                        "parallelism": f"dp{world} (independent env shards, no collective)"},

@@ -107,6 +107,16 @@ TMG_API int tmg_effective(tmg_ctx *ctx, int64_t n, const int8_t *board, uint64_t
 TMG_API int tmg_onehot(tmg_ctx *ctx, int64_t n, const int8_t *board, void *out, int out_dtype, void *stream);
 TMG_API int tmg_onehot_channels(const tmg_ctx *ctx);
 
+/* The examples' policy over info["effective_actions"] (src/examples/q_learning.py:19-25,
+ * qrdqn.py:58), on device: actions[i] uniform over env i's effective actions
+ * (the ascending list of tile_match_env.py:118-124, read from the bitmask eff
+ * [n][W]), picked by a counter-based draw of (key, first_env + i, t) — the
+ * stream of the bench's synthetic actions, so shard layouts agree.  An env with
+ * no effective action gets the uniform draw over all A actions.  Asynchronous
+ * on `stream`. */
+TMG_API int tmg_sample_effective(tmg_ctx *ctx, int64_t n, const uint64_t *eff, uint64_t key, int64_t first_env,
+                                 int32_t t, int32_t *actions, void *stream);
+
 /* Replaces utils.compute_num_states (src/tile_match_gym/utils/utils.py:6-26) on
  * `device`: over all colours^(rows*cols) colourings of an all-normal board,
  * num_line_free = boards with no colour line, num_playable = those that also

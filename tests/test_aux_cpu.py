@@ -46,3 +46,23 @@ def test_onehot_type_slices(cl, co, want):
     """wrappers.py:37-46: kept type slices are sorted(id + 1), ids cookie -1, v 2, h 3, bomb 4."""
     from tile_match_gym_amd.wrappers import _type_slices
     assert list(_type_slices(cl, co)) == want
+
+
+def test_policy_restatement_properties():
+    """The effective-action policy's numpy restatement: picks only effective
+    actions, roughly uniformly, and falls back to the synthetic uniform stream."""
+    from oracle.policy_np import sample_effective_np
+    from tile_match_gym_amd.shard import synthetic_actions
+    rs = np.random.default_rng(5)
+    n, A, W = 4000, 180, 3
+    bits = rs.random((n, W * 64)) < 0.1
+    bits[:, A:] = False
+    bits[:50] = False                                           # no effective action
+    eff = np.packbits(bits, axis=1, bitorder="little").view(np.uint64)
+    a = sample_effective_np(eff, A, 12345, 1000, 7)
+    assert np.all(bits[np.arange(50, n), a[50:]])
+    assert np.array_equal(a[:50], synthetic_actions(range(1000, 1050), 8, A)[7])
+    one = np.zeros((20000, 1), np.uint64)
+    one[:] = np.uint64(0b1011)                                  # actions {0, 1, 3}
+    c = np.bincount(sample_effective_np(one, 64, 9, 0, 0), minlength=4)
+    assert c[2] == 0 and all(abs(c[i] - 20000 / 3) < 400 for i in (0, 1, 3))

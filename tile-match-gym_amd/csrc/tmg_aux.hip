@@ -1,6 +1,7 @@
 // tmg_aux.hip — the callers either side of the Board transition (SURVEY.md
-// §8(f)): the one-hot observation encoding of OneHotWrapper and the
-// brute-force state count of utils.compute_num_states.  Included by
+// §8(d,f)): the one-hot observation encoding of OneHotWrapper, the examples'
+// uniform-over-effective-actions policy and the brute-force state count of
+// utils.compute_num_states.  Included by
 // tmg_capi.hip.  Both are plain HBM-streaming / integer kernels, one thread
 // per (env, cell) and one thread per run of boards respectively.
 
@@ -25,6 +26,45 @@ __global__ __launch_bounds__(256) void onehot_kernel(int64_t n, int N, int k, in
     for (int c = 0; c < k; c++) o[(int64_t)c * N] = (T)(colour == c + 1 ? 1 : 0);
     const int ids[4] = {sel.x, sel.y, sel.z, sel.w};
     for (int j = 0; j < nsel; j++) o[(int64_t)(k + j) * N] = (T)(type == ids[j] ? 1 : 0);
+}
+
+// The examples' policy (src/examples/q_learning.py:19-25: rng.choice over
+// info["effective_actions"]): one action per env, uniform over the env's
+// effective actions (ascending, tile_match_env.py:118-124), from a
+// counter-based draw h = splitmix64(splitmix64(key * K + global env) ^ t * G)
+// — the same stream as shard.synthetic_actions, so any shard layout picks the
+// same actions.  The r-th set bit, r = hi32(h) * count >> 32; with no
+// effective action (a finished env without autoreset) hi32(h) * A >> 32.
+// One thread per env; W <= 16 mask words.
+__device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
+    x += 0x9E3779B97F4A7C15ULL;
+    x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ULL;
+    x = (x ^ (x >> 27)) * 0x94D049BB133111EBULL;
+    return x ^ (x >> 31);
+}
+
+__global__ __launch_bounds__(256) void sample_effective_kernel(int64_t n, int W, int A, const uint64_t *__restrict__ eff,
+                                                               uint64_t key, int64_t first_env, int32_t t,
+                                                               int32_t *__restrict__ actions) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    const uint64_t base = splitmix64(key * 0xD1B54A32D192ED03ULL + (uint64_t)(first_env + i));
+    const uint64_t h = splitmix64(base ^ ((uint64_t)t * 0x9E3779B97F4A7C15ULL)) >> 32;
+    const uint64_t *m = eff + i * W;
+    int count = 0;
+    for (int j = 0; j < W; j++) count += __popcll(m[j]);
+    if (count == 0) { actions[i] = (int32_t)((h * (uint64_t)A) >> 32); return; }
+    int r = (int)((h * (uint64_t)count) >> 32);
+    for (int j = 0; j < W; j++) {
+        uint64_t x = m[j];
+        const int c = __popcll(x);
+        if (r < c) {
+            for (; r > 0; r--) x &= x - 1;              // drop the r lowest set bits
+            actions[i] = j * 64 + (__ffsll((unsigned long long)x) - 1);
+            return;
+        }
+        r -= c;
+    }
 }
 
 // utils.compute_num_states / is_valid_state (src/tile_match_gym/utils/utils.py:6-26):

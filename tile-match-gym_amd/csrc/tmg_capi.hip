@@ -299,6 +299,18 @@ int tmg_onehot(tmg_ctx *ctx, int64_t n, const int8_t *board, void *out, int out_
     return hip_check(hipGetLastError(), "kernel launch");
 }
 
+int tmg_sample_effective(tmg_ctx *ctx, int64_t n, const uint64_t *eff, uint64_t key, int64_t first_env, int32_t t,
+                         int32_t *actions, void *stream) {
+    if (!eff || !actions) return fail(-1, "null buffer");
+    int rc = check_call(ctx, n);
+    if (rc || n == 0) return rc;
+    if (first_env < 0) return fail(-2, "first_env must be >= 0");
+    const dim3 grid((unsigned)((n + 255) / 256)), block(256);
+    hipLaunchKernelGGL(tmg::sample_effective_kernel, grid, block, 0, reinterpret_cast<hipStream_t>(stream), n,
+                       ctx->P.W, ctx->P.A, eff, key, first_env, t, actions);
+    return hip_check(hipGetLastError(), "kernel launch");
+}
+
 int tmg_count_states(int device, int rows, int cols, int colours, uint64_t *num_playable, uint64_t *num_line_free) {
     if (!num_playable || !num_line_free) return fail(-1, "null output pointer");
     if (rows < 1 || cols < 1 || rows * cols > 16) return fail(-2, "count_states needs R*C <= 16");

@@ -14,7 +14,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("TMG_LIB") or os.path.join(_HERE, "_lib", "libtmg.so")   # TMG_LIB: A/B another build
 EXPORTS = ("tmg_create", "tmg_destroy", "tmg_reset", "tmg_step", "tmg_effective",
            "tmg_num_actions", "tmg_mask_words", "tmg_last_error", "tmg_abi_version",
-           "tmg_onehot", "tmg_onehot_channels", "tmg_count_states")
+           "tmg_onehot", "tmg_onehot_channels", "tmg_count_states", "tmg_sample_effective")
 DTYPE_F32, DTYPE_U8, DTYPE_I32 = 0, 1, 2
 ABI_VERSION = 1
 
@@ -54,8 +54,10 @@ def load():
     L.tmg_onehot.argtypes = [P, I64, P, P, I, P]
     L.tmg_onehot_channels.argtypes = [P]
     L.tmg_count_states.argtypes = [I, I, I, I, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64)]
+    L.tmg_sample_effective.argtypes = [P, I64, P, ctypes.c_uint64, I64, ctypes.c_int32, P, P]
     for name in ("tmg_create", "tmg_destroy", "tmg_reset", "tmg_step", "tmg_effective",
                  "tmg_num_actions", "tmg_mask_words", "tmg_abi_version", "tmg_onehot", "tmg_onehot_channels",
+                 "tmg_sample_effective",
                  "tmg_count_states"):
         getattr(L, name).restype = I
     if L.tmg_abi_version() != ABI_VERSION:
@@ -121,6 +123,10 @@ class Context:
 
     def onehot(self, n, board, out, out_dtype, stream):
         check(load().tmg_onehot(self._h, int(n), board, out, int(out_dtype), stream))
+
+    def sample_effective(self, n, eff, key, first_env, t, actions, stream):
+        check(load().tmg_sample_effective(self._h, int(n), eff, int(key) & 0xFFFFFFFFFFFFFFFF, int(first_env),
+                                          int(t), actions, stream))
 
 
 def count_states(device_index: int, rows: int, cols: int, colours: int):

@@ -87,6 +87,7 @@ class TileMatchVecEnv:
         self.n_new = torch.zeros(N, dtype=torch.int32, **kw)
         self.n_act = torch.zeros(N, dtype=torch.int32, **kw)
         self.flags = torch.zeros(N, dtype=torch.uint8, **kw)
+        self.actions = None                     # step_effective's sampled actions (N,) int32
         self._eff_valid = False
         groups = max(1, min(int(groups), N))
         self.groups = groups
@@ -177,6 +178,32 @@ class TileMatchVecEnv:
             for (lo, _), st, p in zip(self._ranges, self._streams, self._gptr):
                 actions_i32.record_stream(st)
                 self.ctx.step(p[0], p[1], p[2], p[3], a0 + 4 * lo, p[5], p[6], p[7], p[8], p[4], trust, auto,
+                              st.cuda_stream)
+        self._eff_valid = True
+
+    def step_effective(self, t: int, key: int = 12345, first_env: int = 0):
+        """Enqueue one step of the examples' policy (src/examples/q_learning.py:19-25):
+        every env takes an action drawn uniformly from its effective actions
+        (tmg_sample_effective; counter-based in (key, first_env + env, t), so a
+        shard passing its global offset as first_env picks the same actions as
+        the unsharded batch).  The sampled actions stay in self.actions."""
+        if not self._eff_valid:
+            self.compute_effective()
+        if self.actions is None:
+            self.actions = torch.zeros(self.num_envs, dtype=torch.int32, device=self.device)
+        trust, auto = 1, int(self.autoreset)
+        act = self.actions.data_ptr()
+        if not self._streams:
+            s = self._stream()
+            self.ctx.sample_effective(self.num_envs, _ptr(self.eff), key, first_env, t, act, s)
+            self.ctx.step(self.num_envs, _ptr(self.board), _ptr(self.rng), _ptr(self.timer), act,
+                          _ptr(self.reward), _ptr(self.n_new), _ptr(self.n_act), _ptr(self.flags), _ptr(self.eff),
+                          trust, auto, s)
+        else:
+            self._fork()
+            for (lo, _), st, p in zip(self._ranges, self._streams, self._gptr):
+                self.ctx.sample_effective(p[0], p[4], key, first_env + lo, t, act + 4 * lo, st.cuda_stream)
+                self.ctx.step(p[0], p[1], p[2], p[3], act + 4 * lo, p[5], p[6], p[7], p[8], p[4], trust, auto,
                               st.cuda_stream)
         self._eff_valid = True
 
