@@ -198,7 +198,7 @@ def main():
                        "specials": cl + co, "env_groups_per_gpu": env.groups,
                        "parallelism": f"dp{world} (independent env shards, no collective)"},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(achieved / HBM_PEAK_GBS, 6), "traffic": load_traffic(args.config),
+                         "frac": round(achieved / HBM_PEAK_GBS, 6), "traffic": load_traffic(args.config) if args.policy == "uniform" else None,
                          "kernel_ms_per_launch": round(kern_ms, 4), "envs_per_launch": launch_envs,
                          "algorithmic_bytes_per_env_step": bpu,
                          "job_gbs": round(bpu * nb * args.steps / el / 1e9, 2)},
