@@ -30,6 +30,11 @@ __device__ __forceinline__ int ctz64(uint64_t x) { return __ffsll((unsigned long
 #define TMG_CONST_AS __attribute__((address_space(4)))
 #endif
 typedef const TMG_CONST_AS uint64_t sbrow_t;
+
+// an empty asm that reads three VGPR values: they must exist at this point
+#ifndef TMG_KEEP_V3
+#define TMG_KEEP_V3(x, y, z) asm volatile("" ::"v"(x), "v"(y), "v"(z))
+#endif
 __device__ __forceinline__ Pair sb_row(const Params &P, int r) {           // cells of row r
     const sbrow_t *t = (const sbrow_t *)P.sb_rows + 4 * r;
     return Pair{t[0], t[1]};
@@ -133,19 +138,27 @@ __device__ __forceinline__ int sb_bottom_row(const Params &P, const SBDet &d) {
 // the cells' (row << 8 | 255 - col) << 1, -1 outside the board) by one DPP
 // max.  A vertical line starts at the top of its run (:166-172).
 template <int NB, bool CODD>
-__device__ __forceinline__ int sb_first_line_row(const Params &P, const SB<NB> &s, int lane, int keyA, int keyB) {
-    const SBDet d = sb_detect<NB, CODD>(P, s);
+__device__ __forceinline__ int sb_first_line_key(const Params &P, const SBDet &d, int lane, int keyA, int keyB) {
+    (void)P;
     const int vA = (int)(d.va.a >> lane) & 1, hA = (int)(d.ha.a >> lane) & 1;
     const int vB = (int)(d.va.b >> lane) & 1, hB = (int)(d.ha.b >> lane) & 1;
     const int ka = (vA | hA) ? keyA | vA : -1, kb = (vB | hB) ? keyB | vB : -1;
-    const int key = wave_max(ka > kb ? ka : kb);
-    if (key < 0) return -1;
+    return wave_max(ka > kb ? ka : kb);
+}
+template <bool CODD>
+__device__ __forceinline__ int sb_line_row_of_key(const Params &P, const SBDet &d, int key) {   // key >= 0
     const int rs = key >> 9;
     if (!(key & 1)) return rs;
     const int C = P.C;
     int t = (rs - 2) * C + 255 - ((key >> 1) & 255);
     while (t >= C && !test(d.neU, t)) t -= C;
     return div_c(P, t);
+}
+template <int NB, bool CODD>
+__device__ __forceinline__ int sb_first_line_row(const Params &P, const SB<NB> &s, int lane, int keyA, int keyB) {
+    const SBDet d = sb_detect<NB, CODD>(P, s);
+    const int key = sb_first_line_key<NB, CODD>(P, d, lane, keyA, keyB);
+    return key < 0 ? -1 : sb_line_row_of_key<CODD>(P, d, key);
 }
 
 // the keys of sb_first_line_row for cells 2*lane, 2*lane+1
@@ -306,9 +319,21 @@ __device__ __forceinline__ void sb_gravity_refill(const Params &P, WS &w, int la
 // output j by jump-ahead (as draw_colours; M <= 128 is one 64-output pass)
 // and keeps the two colours of its own cells: output j holds draws 2j and
 // 2j+1, or, after a buffered half-word (draw 0), draws 2j+1 and 2j+2.
+// The batch's jump-ahead depends only on the stream position, not on the row:
+// remove_colour_lines computes it before the line search of the board it
+// replaces, so the VALU chain issues beside that search's SALU work.
+struct SBDrawPre {
+    U128 sj;
+    uint64_t out;
+};
+__device__ __forceinline__ SBDrawPre sb_draw_pre(const LaneJump &J, const Rng &g) {
+    const U128 sj = add128(mul128(J.Aj, U128{g.slo, g.shi}), J.incG);
+    return SBDrawPre{sj, xsl_rr(sj)};
+}
+
 template <int NB, class WS>
 __device__ __forceinline__ void sb_draw_rows(const Params &P, WS &w, int lane, const LaneJump &J, Rng &g, int row,
-                                             SBC &c) {
+                                             SBC &c, const SBDrawPre &pre) {
     const uint32_t k = (uint32_t)P.k;
     const int M = (row + 1) * P.C;
     const bool inA = 2 * lane < M, inB = 2 * lane + 1 < M;
@@ -322,8 +347,8 @@ __device__ __forceinline__ void sb_draw_rows(const Params &P, WS &w, int lane, c
     const bool rbuf = off && (uint32_t)mbuf < P.thr;
     const int need = M - off;
     const int n64 = (need + 1) >> 1;
-    const U128 sj = add128(mul128(J.Aj, U128{g.slo, g.shi}), J.incG);
-    const uint64_t out = xsl_rr(sj);
+    const U128 sj = pre.sj;
+    const uint64_t out = pre.out;
     const uint64_t m0 = (uint64_t)(uint32_t)out * k, m1 = (out >> 32) * k;
     const bool ok0 = lane < n64, ok1 = 2 * lane + 1 < need;
     const bool rej = (ok0 && (uint32_t)m0 < P.thr) || (ok1 && (uint32_t)m1 < P.thr);
@@ -362,10 +387,15 @@ __device__ __forceinline__ bool sb_ensure(const Params &P, WS &w, int lane, cons
     for (;;) {
         if (!clean) {
             for (;;) {
-                const int r0 = sb_first_line_row<NB, CODD>(P, sb_planes_of<NB>(c), lane, keyA, keyB);
-                if (r0 < 0) break;
+                const SBDrawPre pre = sb_draw_pre(J, g);
+                const SBDet d = sb_detect<NB, CODD>(P, sb_planes_of<NB>(c));
+                const int key = sb_first_line_key<NB, CODD>(P, d, lane, keyA, keyB);
+                // keep the jump-ahead above the exit test (else it is sunk below it)
+                TMG_KEEP_V3(pre.sj.lo, pre.sj.hi, pre.out);
+                if (key < 0) break;
+                const int r0 = sb_line_row_of_key<CODD>(P, d, key);
                 const int row = P.R - 1 < r0 + 1 ? P.R - 1 : r0 + 1;   // colour plane only, rows 0..row
-                sb_draw_rows<NB>(P, w, lane, J, g, row, c);
+                sb_draw_rows<NB>(P, w, lane, J, g, row, c, pre);
                 dirty = true;
             }
         }
@@ -391,7 +421,7 @@ template <int NB, bool CODD, class WS>
 __device__ __forceinline__ void sb_generate(const Params &P, WS &w, int lane, const LaneJump &J, Rng &g,
                                             const Cells<WS::NP> &cl) {
     SBC c{0, 0};
-    sb_draw_rows<NB>(P, w, lane, J, g, P.R - 1, c);
+    sb_draw_rows<NB>(P, w, lane, J, g, P.R - 1, c, sb_draw_pre(J, g));
     for (int p = lane; p < P.N; p += 64) w.brd[P.N + p] = 1;
     sb_ensure<NB, CODD>(P, w, lane, J, g, cl, c, true, false);
 }

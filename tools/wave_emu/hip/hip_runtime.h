@@ -57,4 +57,5 @@ inline unsigned max(unsigned a, unsigned b) { return a > b ? a : b; }
 inline uint64_t __builtin_amdgcn_s_memrealtime() { return 0; }
 
 #define TMG_CONST_AS
+#define TMG_KEEP_V3(x, y, z) ((void)0)
 #define TMG_SMEM_DECL(name) unsigned char *name = emu_smem()
