@@ -39,8 +39,9 @@ inline int emu_update_dpp(int old, int src, int ctrl, int row_mask, int bank_mas
     return (int)(uint32_t)emu_collective(EMU_DPP, v, ctrl | (row_mask << 12) | (bank_mask << 16) | ((bound_ctrl ? 1 : 0) << 20));
 }
 #define __builtin_amdgcn_update_dpp(o, s, c, r, b, bc) emu_update_dpp((o), (s), (c), (r), (b), (bc))
-#define __builtin_amdgcn_readlane(v, l) emu_readlane((v), (l))
-#define __builtin_amdgcn_readfirstlane(v) emu_readfirstlane(v)
+// the builtin returns int (an OR into a 64-bit value sign-extends it, as on the device)
+#define __builtin_amdgcn_readlane(v, l) ((int)emu_readlane((uint32_t)(v), (l)))
+#define __builtin_amdgcn_readfirstlane(v) ((int)emu_readlane((uint32_t)(v), 0))
 #define __builtin_amdgcn_fence(order, scope) emu_sync()
 #define __builtin_amdgcn_wave_barrier() ((void)0)
 inline void __syncthreads() { emu_sync(); }
