@@ -607,14 +607,21 @@ __device__ __forceinline__ int run_top(const Params &P, const WS &w, int lane, i
 // columns left to right with the vertical check first; so the first line is
 // the maximum of key = (row, -col, is_vertical) over anchor cells: one DPP
 // max-reduction instead of mask bookkeeping.
+//
+// lim: no anchor lies below row lim.  The 64-cell passes are scanned from the
+// one holding row lim's last cell upwards and the scan stops one pass above
+// the first pass holding an anchor: the bottom-most anchor row (C <= 64
+// cells) lies in that pass and the one above it.  ra: the anchor row found.
 template <class WS>
-__device__ __forceinline__ int first_line_row(const Params &P, const WS &w, int lane, const Cells<WS::NP> &cl) {
+__device__ __forceinline__ int first_line_row(const Params &P, const WS &w, int lane, const Cells<WS::NP> &cl,
+                                              int lim, int &ra) {
     const int C = P.C, N = P.N, N1 = P.N - 1;
     const int8_t *col = w.brd, *typ = w.brd + N;
-    int best = -1;
+    const int last = min((lim + 1) * C, N) - 1;          // highest cell that may anchor a line
+    int best = -1, stop = -2;                            // stop: lowest pass still to scan, once found
 #pragma unroll
-    for (int i = 0; i < WS::NP; i++) {
-        if (i * 64 >= N) continue;
+    for (int i = WS::NP - 1; i >= 0; i--) {
+        if (i * 64 > last || i < stop) continue;         // wave-uniform
         const int p = i * 64 + lane;
         const int pc = min(p, N1);
         const int x = col[pc];
@@ -625,10 +632,12 @@ __device__ __forceinline__ int first_line_row(const Params &P, const WS &w, int 
         const uint32_t hb = cl.hbad[i] | tbad | ne(h1, x) | ne(h2, x);
         const int base = ((cl.r[i] << 8) | (255 - cl.c[i])) << 1;
         best = max(best, max(vb == 0 ? base | 1 : -1, hb == 0 ? base : -1));
+        if (stop == -2 && __ballot(best >= 0) != 0ULL) stop = i - 1;
     }
+    if (stop == -2) return -1;
     const int key = wave_max(best);
-    if (key < 0) return -1;
     const int rs = key >> 9;
+    ra = rs;
     if (!(key & 1)) return rs;                            // horizontal line at (rs, c0..)
     const int c0 = 255 - ((key >> 1) & 255);
     return run_top(P, w, lane, rs, c0);                   // vertical: starts at the top of its run
@@ -730,12 +739,17 @@ __device__ __forceinline__ bool ensure_playable(const Params &P, WS &w, int lane
                                 const Cells<WS::NP> &cl) {
     bool shuffled = false;
     for (;;) {
+        // Redrawing rows 0..row leaves every cell an anchor test reads in rows
+        // > row + 2 unchanged, so after it no anchor lies below max(row + 2, ra).
+        int lim = P.R - 1;
         for (;;) {
-            int r0 = first_line_row(P, w, lane, cl);
+            int ra = 0;
+            int r0 = first_line_row(P, w, lane, cl, lim, ra);
             if (r0 < 0) break;
             int row = P.R - 1 < r0 + 1 ? P.R - 1 : r0 + 1;   // colour plane only, rows 0..row
             draw_colours(P, lane, J, g, (row + 1) * P.C, w.brd, w.trash);
             WSYNC();
+            lim = min(P.R - 1, max(row + 2, ra));
         }
         if (scan_effective(P, w, lane, cl, (P.smask & SP_COOKIE) == 0)) break;
         WSYNC();
