@@ -139,6 +139,9 @@ def test_generate_golden_gpu():
     (10, 10, 4, 0, 8192, 65),
     (10, 10, 4, 14, 4096, 65),
     (20, 20, 6, 15, 512, 35),
+    # 512-cell path, rows straddling the 64-cell passes unevenly (bounded line search)
+    (16, 24, 7, 0, 256, 35),
+    (24, 21, 7, 9, 256, 35),
     (8, 8, 3, 15, 4096, 65),
     (5, 5, 3, 15, 4096, 65),
     (6, 7, 5, 1, 2048, 45),
