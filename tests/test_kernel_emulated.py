@@ -59,6 +59,8 @@ def test_trajectory_golden_emulated(emu_lib, name, autoreset, monkeypatch):
     # 128 cells, C = 63) and the general kernel with specials
     (10, 10, 4, 0), (8, 8, 3, 0), (7, 5, 5, 0), (6, 9, 9, 0), (3, 4, 2, 0), (16, 8, 4, 0), (2, 63, 6, 0),
     (11, 11, 4, 0), (10, 10, 4, 14), (8, 8, 3, 15), (5, 12, 6, 15),
+    # 512-cell kernels: rows straddle the 64-cell passes unevenly (bounded line search)
+    (16, 24, 7, 0), (24, 21, 7, 9),
 ])
 def test_random_rollouts_emulated(emu_lib, cfg):
     """Random-action rollouts with autoreset: emulated kernels vs the oracle, every field, every step."""
