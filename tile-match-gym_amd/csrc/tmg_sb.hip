@@ -130,8 +130,9 @@ __device__ __forceinline__ int sb_bottom_row(const Params &P, const SBDet &d) {
     return pm < 0 ? -1 : div_c(P, pm);
 }
 
-// remove_colour_lines (board.py:120-131): row of the first coord of the first
-// line get_colour_lines returns, or -1.  get_colour_lines scans rows
+// remove_colour_lines (board.py:120-131) needs the row of the first coord of
+// the first line get_colour_lines returns: sb_first_line_key gives that line's
+// key (or -1: no line), sb_line_row_of_key the row.  get_colour_lines scans rows
 // bottom-up and, in the first row holding a line, columns left to right with
 // the vertical check first; so the first line is the maximum over anchor
 // cells of key = (row, -col, is_vertical), taken lane-parallel (keyA/keyB:
@@ -154,14 +155,7 @@ __device__ __forceinline__ int sb_line_row_of_key(const Params &P, const SBDet &
     while (t >= C && !test(d.neU, t)) t -= C;
     return div_c(P, t);
 }
-template <int NB, bool CODD>
-__device__ __forceinline__ int sb_first_line_row(const Params &P, const SB<NB> &s, int lane, int keyA, int keyB) {
-    const SBDet d = sb_detect<NB, CODD>(P, s);
-    const int key = sb_first_line_key<NB, CODD>(P, d, lane, keyA, keyB);
-    return key < 0 ? -1 : sb_line_row_of_key<CODD>(P, d, key);
-}
-
-// the keys of sb_first_line_row for cells 2*lane, 2*lane+1
+// the keys of sb_first_line_key for cells 2*lane, 2*lane+1
 __device__ __forceinline__ void sb_line_keys(const Params &P, int lane, int &keyA, int &keyB) {
     const int q0 = 2 * lane, q1 = q0 + 1;
     const int r0 = div_c(P, q0), r1 = div_c(P, q1);
