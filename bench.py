@@ -6,16 +6,28 @@
 One "step" = one TileMatchEnv.step for every env of the shard (one HIP launch
 per env group; `--groups` groups run on separate HIP streams so one group's
 launch tail overlaps the next group's launch — same boards, same work),
-uniform random actions pre-staged in HBM, autoreset on (num_moves = 30, so
-every 30th step also regenerates every board).  Each rank steps its own
-contiguous shard of envs (seed = global env index); there is no collective on
-the data path.  Rank 0 prints one JSON line.
+uniform random actions pre-staged in HBM, autoreset on (num_moves = 30).
+
+Episode phases are staggered after the reset (`TileMatchVecEnv.stagger_phases`:
+env i starts at timer (global i) mod 30, the state of i mod 30 ineffective
+moves), so every step of any timed window finishes ~1/30 of the episodes and
+regenerates those boards (tile_match_env.py:84-91 -> board.py:95-131): the
+amortised work of the aligned run, whatever --steps / --warmup are.
+
+Multi-GPU: one process per GPU, each stepping its own contiguous shard of envs
+(seed = global env index); there is no collective on the data path, only a
+barrier around the timed region and a MAX of the elapsed time (gloo, on the
+host).  Under torch.distributed.run the ranks come from the environment; a
+plain `--gpus N` (N > 1) spawns the N rank processes itself before anything
+touches the GPU.  Rank 0 prints one JSON line.
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -24,11 +36,14 @@ for _p in (ROOT, os.path.join(ROOT, "tile-match-gym_amd")):
     if _p not in sys.path:
         sys.path.insert(0, _p)
 
-import numpy as np  # noqa: E402
-import torch  # noqa: E402
-
 METRIC = "env-steps/sec (whole node), 65536×10×10 boards, at 1/2/4/8 MI355X"
-HBM_PEAK_GBS = 8000.0           # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+HBM_PEAK_GBS = 8000.0           # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip-level parameters)
+# Issue peaks (MI355X_MICROARCH.md: 256 CUs x 4 SIMD-32, 2.4 GHz; a wave64 VALU
+# instruction takes 2 cycles of its SIMD; one scalar unit per CU issuing at
+# most one SALU instruction per cycle), in wave-instructions per second.
+CLOCK_HZ = 2.4e9
+VALU_PEAK = 256 * 4 * CLOCK_HZ / 2
+SALU_PEAK = 256 * CLOCK_HZ
 
 CONFIGS = {
     # name: (R, C, k, colourless, colour, boards per GPU, description)
@@ -38,6 +53,9 @@ CONFIGS = {
     "c5": (20, 20, 6, ["cookie"], ["vertical_laser", "horizontal_laser", "bomb"], 262144,
            "262144 x 20x20 boards per GPU, 6 colours, all specials"),
 }
+# The reference's own Python step() measured in the survey container (BASELINE.md §2,
+# 8 vCPU Xeon, numba absent): context for the CPU baseline, not a target.
+REF_PY = {"c2": (290, 1976), "c3": (281, 2421), "c5": (69, 492)}
 
 
 def algorithmic_bytes_per_env_step(R, C):
@@ -48,27 +66,34 @@ def algorithmic_bytes_per_env_step(R, C):
     return 4 * R * C + 48 + 8 + 4 + 8 + 16 + 8 * ((A + 63) // 64)
 
 
-def cpu_baseline(R, C, k, smask, moves, budget_s=12.0, policy="uniform"):
-    """The oracle (oracle/tmg_oracle.c, a bit-exact C port of the reference
-    Board) timed on this host's cores over a bounded sample of the same
-    workload (same seeds / action distribution; for the effective-action policy
-    the numpy restatement of the sampler picks the actions, inside the timing)."""
+def host_threads():
+    """Host cores this job may use: the affinity set, capped by OMP_NUM_THREADS
+    when the launcher sets it (the GPU box gives each GPU a 16-core share)."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    omp = os.environ.get("OMP_NUM_THREADS")
+    if omp and omp.isdigit() and int(omp) > 0:
+        n = min(n, int(omp))
+    return max(1, n)
+
+
+def _time_oracle(R, C, k, smask, moves, n, threads, budget_s, policy):
+    import numpy as np
     from oracle import oracle as orc
     from tile_match_gym_amd.seeding import batch_rng_words
-    threads = min(16, os.cpu_count() or 1)
-    n = 2048
+    from tile_match_gym_amd.shard import synthetic_actions
+    A = 2 * R * C - R - C
     o = orc.OracleBatch(R, C, k, smask, moves, batch_rng_words(range(n)), threads=threads)
     o.reset()
-    from tile_match_gym_amd.shard import synthetic_actions
+    o.timer[:] = np.arange(n) % moves              # the bench's staggered phases
     T = 300
-    acts = synthetic_actions(range(n), T, 2 * R * C - R - C)
+    acts = synthetic_actions(range(n), T, A)
     steps = 0
     t0 = time.perf_counter()
     while True:
         for t in range(moves):
             if policy == "effective":
                 from oracle.policy_np import sample_effective_np
-                a = sample_effective_np(o.eff, 2 * R * C - R - C, 12345, 0, steps + t)
+                a = sample_effective_np(o.eff, A, 12345, 0, steps + t)
             else:
                 a = acts[(steps + t) % T]
             o.step(a, autoreset=True)
@@ -76,20 +101,54 @@ def cpu_baseline(R, C, k, smask, moves, budget_s=12.0, policy="uniform"):
         el = time.perf_counter() - t0
         if el >= budget_s:
             break
-    return {"value": round(n * steps / el, 1), "unit": "env-steps/s", "cores": threads, "kind": "port",
-            "sample": f"{n} envs x {steps} steps ({steps // moves} episodes incl. autoreset), "
-                      f"{el:.1f} s, OpenMP over {threads} threads"}
+    return n * steps / el, steps, el
 
 
-def load_traffic(config):
-    p = os.path.join(ROOT, "profiles", "traffic.json")
+def cpu_baseline(config, R, C, k, smask, moves, policy="uniform"):
+    """The oracle (oracle/tmg_oracle.c, a bit-exact C restatement of the
+    reference Board) timed on this host over a bounded sample of the same
+    workload (same seeds, staggered phases and action stream): once on one
+    thread and once over every host core this job may use (OpenMP)."""
+    threads = host_threads()
+    single, s_steps, s_el = _time_oracle(R, C, k, smask, moves, 256, 1, 8.0, policy)
+    multi, m_steps, m_el = _time_oracle(R, C, k, smask, moves, 256 * threads, threads, 8.0, policy)
+    ref1, ref8 = REF_PY.get(config, (None, None))
+    return {"value": round(multi, 1), "unit": "env-steps/s", "cores": threads, "kind": "port",
+            "sample": f"{256 * threads} envs x {m_steps} steps ({m_steps // moves} episodes incl. autoreset), "
+                      f"{m_el:.1f} s, OpenMP over {threads} threads",
+            "single_thread": {"value": round(single, 1), "cores": 1,
+                              "sample": f"256 envs x {s_steps} steps, {s_el:.1f} s"},
+            "reference_python_survey": {"value_1_process": ref1, "value_8_processes": ref8,
+                                        "note": "reference TileMatchEnv.step, survey container 8 vCPU, numba absent "
+                                                "(BASELINE.md §2); context only"}}
+
+
+def load_profile(name, config):
+    p = os.path.join(ROOT, "profiles", name)
     if not os.path.exists(p):
         return None
     try:
-        d = json.load(open(p))
-        return d.get(config, {}).get("hbm_bytes_per_launch")
+        with open(p) as f:
+            return json.load(f).get(config)
     except Exception:
         return None
+
+
+def spawn_ranks(n):
+    """`bench.py --gpus n` without a launcher: start n rank processes (this
+    process touches no GPU) and exit with the worst of their codes."""
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    rc = 0
+    for p in procs:
+        rc = max(rc, p.wait())
+    return rc
 
 
 def main():
@@ -104,38 +163,50 @@ def main():
     ap.add_argument("--policy", default="uniform", choices=("uniform", "effective"),
                     help="uniform: random actions over all A (headline); effective: every env samples uniformly "
                          "from its effective actions on device each step (SURVEY §8(d) secondary mode)")
+    ap.add_argument("--no-stagger", action="store_true", help="aligned episodes (every env resets on the same step)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--dry-run", action="store_true", help="print each rank's shard layout and exit (no GPU)")
     args = ap.parse_args()
 
     from tile_match_gym_amd.shard import dist_env, max_over_ranks, shard_range, shard_seeds, synthetic_actions
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(spawn_ranks(args.gpus))
     world, rank, local_rank = dist_env()
-    dist = None
-    if world > 1:
-        import torch.distributed as dist
-        # one process per GPU; TMG_DIST_BACKEND=gloo rehearses the N>1 path with
-        # several ranks on one device (RCCL refuses duplicate GPUs)
-        torch.cuda.set_device(local_rank % torch.cuda.device_count())
-        dist.init_process_group(os.environ.get("TMG_DIST_BACKEND", "nccl"))
-    else:
-        torch.cuda.set_device(0)
-    dev = torch.device("cuda", torch.cuda.current_device())
-
-    from tile_match_gym_amd.vec_env import TileMatchVecEnv
     R, C, k, cl, co, nb, desc = CONFIGS[args.config]
     if args.boards:
         nb = args.boards
+    rng_ = shard_range(rank, nb)
+    if args.dry_run:
+        print(json.dumps({"rank": rank, "world": world, "local_rank": local_rank, "envs": [rng_.start, rng_.stop]}),
+              flush=True)
+        return
+
+    import torch
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        # one process per GPU; the only collectives (a barrier and a MAX of the
+        # elapsed time) run on the host
+        dist.init_process_group(os.environ.get("TMG_DIST_BACKEND", "gloo"))
+    ndev = torch.cuda.device_count()
+    torch.cuda.set_device(local_rank % max(1, ndev))
+    dev = torch.device("cuda", torch.cuda.current_device())
+
+    from tile_match_gym_amd.vec_env import TileMatchVecEnv
     moves = 30
     env = TileMatchVecEnv(nb, R, C, k, moves, cl, co, seeds=shard_seeds(rank, nb), device=dev, autoreset=True,
                           groups=args.groups)
     A = env.num_actions
     T = 300
-    acts = torch.from_numpy(synthetic_actions(shard_range(rank, nb), T, A)).to(dev)
+    acts = torch.from_numpy(synthetic_actions(rng_, T, A)).to(dev)
     env.reset()
-    first_env = shard_range(rank, nb).start
+    if not args.no_stagger:
+        env.stagger_phases(first_env=rng_.start)
+    env.status(clear=True)
 
     def step(t):
         if args.policy == "effective":
-            env.step_effective(t, first_env=first_env)       # sampler + step, both on device
+            env.step_effective(t, first_env=rng_.start)       # sampler + step, both on device
         else:
             env.step_raw(acts[t % T])
 
@@ -144,38 +215,56 @@ def main():
     env.join()
     torch.cuda.synchronize()
 
-    # HIP events on the stream the first env group's kernels are launched on,
-    # bracketing the timed region: its back-to-back launches' average duration
-    # (the dominant kernel's per-launch time for the roofline)
-    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    # HIP events: on the current stream around the whole step (fork ... join:
+    # the device time of a step, all groups), and on group 0's stream (its
+    # launches' average duration, comparable with rocprofv3's per-kernel stats)
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    env.record(ev0)
+    ev[0].record()
+    env.record(ev[2])
     for i in range(args.steps):
         step(args.warmup + i)
-    env.record(ev1)
+    env.record(ev[3])
     env.join()
+    ev[1].record()
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
     el = time.perf_counter() - t0
-    kern_ms = ev0.elapsed_time(ev1) / max(1, args.steps)
+    step_ms = ev[0].elapsed_time(ev[1]) / max(1, args.steps)
+    kern_ms = ev[2].elapsed_time(ev[3]) / max(1, args.steps)
     launch_envs = env._ranges[0][1] - env._ranges[0][0]
-    flags = env.flags.cpu().numpy()
-    assert not (flags & 0xC0).any(), "error/overflow flag raised during the bench"
+    st = env.status()                     # sticky: every env of every step, warmup included
+    if st & 0x3:
+        raise SystemExit(f"bench: internal error / overflow raised during the run (status {st:#x})")
     el = max_over_ranks(el, dist, dev)
+    step_ms = max_over_ranks(step_ms, dist, dev)
     kern_ms = max_over_ranks(kern_ms, dist, dev)
 
     if rank == 0:
         total = nb * world * args.steps
         value = total / el
         bpu = algorithmic_bytes_per_env_step(R, C)
-        achieved = bpu * launch_envs / (kern_ms * 1e-3) / 1e9
+        achieved = bpu * nb / (step_ms * 1e-3) / 1e9          # one GPU's envs per step / its device time per step
         smask = (1 if "cookie" in cl else 0) | (2 if "vertical_laser" in co else 0) | \
                 (4 if "horizontal_laser" in co else 0) | (8 if "bomb" in co else 0)
-        cpu = None if (args.no_cpu_baseline or world > 1) else cpu_baseline(R, C, k, smask, moves, policy=args.policy)
+        cpu = None if (args.no_cpu_baseline or world > 1) else cpu_baseline(args.config, R, C, k, smask, moves,
+                                                                             policy=args.policy)
+        issue = None
+        prof = load_profile("issue.json", args.config) if args.policy == "uniform" else None
+        if prof:
+            per_gpu = value / world
+            v = prof["valu_per_env_step"] * per_gpu
+            s = prof["salu_per_env_step"] * per_gpu
+            issue = {"valu_per_env_step": prof["valu_per_env_step"], "salu_per_env_step": prof["salu_per_env_step"],
+                     "valu_rate": round(v, 1), "salu_rate": round(s, 1), "valu_peak": VALU_PEAK,
+                     "salu_peak": SALU_PEAK, "unit": "wave-instructions/s per GPU",
+                     "valu_frac": round(v / VALU_PEAK, 4), "salu_frac": round(s / SALU_PEAK, 4),
+                     "source": prof.get("source")}
+        traffic = load_profile("traffic.json", args.config) if args.policy == "uniform" else None
         out = {
             "metric": METRIC,
             "value": round(value, 1),
@@ -193,15 +282,18 @@ def main():
                      "synthetic (each step every env samples uniformly from its effective actions on device, "
                      "counter-based per (step, global env); seeds = global env index)"),
             "config": {"workload": f"{args.config}: {desc}, num_moves=30, autoreset"
+                                   + ("" if args.no_stagger else ", episode phases staggered (timer0 = env mod 30)")
                                    + ("" if args.policy == "uniform" else ", effective-action policy"),
                        "boards_per_gpu": nb, "rows": R, "cols": C, "colours": k,
                        "specials": cl + co, "env_groups_per_gpu": env.groups,
                        "parallelism": f"dp{world} (independent env shards, no collective)"},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(achieved / HBM_PEAK_GBS, 6), "traffic": load_traffic(args.config) if args.policy == "uniform" else None,
+                         "frac": round(achieved / HBM_PEAK_GBS, 6),
+                         "traffic": traffic.get("hbm_bytes_per_launch") if traffic else None,
+                         "algorithmic_bytes_per_env_step": bpu, "device_ms_per_step": round(step_ms, 4),
                          "kernel_ms_per_launch": round(kern_ms, 4), "envs_per_launch": launch_envs,
-                         "algorithmic_bytes_per_env_step": bpu,
-                         "job_gbs": round(bpu * nb * args.steps / el / 1e9, 2)},
+                         "per_launch_gbs": round(bpu * launch_envs / (kern_ms * 1e-3) / 1e9, 2),
+                         "issue": issue},
             "cpu_baseline": cpu,
         }
         print(json.dumps(out), flush=True)

@@ -125,6 +125,23 @@ TMG_API int tmg_sample_effective(tmg_ctx *ctx, int64_t n, const uint64_t *eff, u
 TMG_API int tmg_count_states(int device, int rows, int cols, int colours, uint64_t *num_playable,
                              uint64_t *num_line_free);
 
+/* Sticky status of the context: the OR, over every env of every call since
+ * the last clear, of TMG_STATUS_INTERNAL (a safety cap or an inconsistent
+ * board ended a step with TMG_FLAG_ERROR), TMG_STATUS_OVERFLOW (a step met
+ * TMG_FLAG_OVERFLOW) and TMG_STATUS_CALLER (a step after done / a bad action).
+ * Waits for the device; clear != 0 then zeroes it.  The reference raises at
+ * the point of failure (tile_match_env.py:94-95, board.py:349-350); a batch
+ * reports through this word and the per-env flags instead. */
+#define TMG_STATUS_INTERNAL 1u
+#define TMG_STATUS_OVERFLOW 2u
+#define TMG_STATUS_CALLER   4u
+TMG_API int tmg_status(tmg_ctx *ctx, uint32_t *status, int clear);
+
+/* 1 when some rows x cols board with `colours` colours is line-free and has an
+ * effective move, i.e. the reference's generate_board terminates
+ * (board.py:102-109); tmg_create refuses the other shapes. */
+TMG_API int tmg_viable(int rows, int cols, int colours);
+
 /* Number of actions A = 2RC - R - C (tile_match_env.py:58) and mask words W. */
 TMG_API int tmg_num_actions(const tmg_ctx *ctx);
 TMG_API int tmg_mask_words(const tmg_ctx *ctx);

@@ -69,3 +69,29 @@ def test_seeding_matches_numpy():
         g1 = np.random.default_rng(s)
         g2 = generator_from_words(rng_words_from_seed(s))
         assert np.array_equal(g1.integers(1, 7, 50), g2.integers(1, 7, 50))
+
+
+def test_viability_matches_state_counts():
+    """tmg_viable (the tmg_create guard) == "some board is line-free and
+    playable", i.e. compute_num_states' playable count > 0 (oracle restatement
+    of utils.py:6-26, pinned by tests/golden/fn_count_states.npz)."""
+    from oracle import oracle as orc
+    from tile_match_gym_amd import _native
+    for R in range(1, 5):
+        for C in range(1, 5):
+            for k in (1, 2, 3):
+                if k ** (R * C) > 600_000:
+                    continue
+                playable, _ = orc.count_states(R, C, k)
+                assert _native.viable(R, C, k) == (playable > 0), (R, C, k, playable)
+    for shape in ((10, 10, 4), (20, 20, 6), (8, 8, 3), (1, 13, 2), (2, 64, 2), (64, 8, 15)):
+        assert _native.viable(*shape), shape
+
+
+def test_create_refuses_unplayable_shapes():
+    """Shapes whose generate_board loop (board.py:102-109) never ends are
+    refused at creation instead of hanging a wave."""
+    from tile_match_gym_amd import _native
+    for shape in ((2, 2, 4), (3, 3, 1), (1, 3, 5), (2, 2, 2)):
+        with pytest.raises(_native.TmgError, match="no playable board"):
+            _native.Context(0, shape[0], shape[1], shape[2], 0, 30)

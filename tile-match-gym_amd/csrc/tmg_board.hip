@@ -63,6 +63,19 @@ namespace tmg {
 enum : int { SP_COOKIE = 1, SP_VLASER = 2, SP_HLASER = 4, SP_BOMB = 8 };
 enum : int { M_NORMAL = 0, M_VLASER = 1, M_HLASER = 2, M_BOMB = 3, M_COOKIE = 4 };
 enum : int { FL_DONE = 1, FL_COMBO = 2, FL_SHUF = 4, FL_RESET = 8, FL_OVF = 0x40, FL_ERR = 0x80 };
+// sticky status word (tmg_status): OR of what any env met since the last clear
+enum : uint32_t { ST_INTERNAL = 1, ST_OVERFLOW = 2, ST_CALLER = 4 };
+
+// Safety caps of the "while not possible_move() or lines" loop (board.py:102-109,
+// 381-391).  tmg_create rejects shapes on which no playable board exists, so a
+// real board never comes near them; reaching one ends the loop with FL_ERR
+// instead of spinning the wave forever (the reference would spin).
+#ifndef TMG_MAX_REDRAWS
+#define TMG_MAX_REDRAWS (1 << 20)    // remove_colour_lines calls per loop
+#endif
+#ifndef TMG_MAX_SHUFFLES
+#define TMG_MAX_SHUFFLES (1 << 12)   // shuffles per loop
+#endif
 
 struct Params {
     int R, C, N, A, W, k, smask, num_moves;
@@ -77,6 +90,7 @@ struct Params {
     uint64_t sb_z;                // one column's cells of one word, from bit 0
     uint64_t sb_in[2], sb_u[2], sb_v[2];   // cells of the board / of rows >= 1 / of rows >= 2
     const uint64_t *sb_rows;      // [R][4]: row r's cells (a, b), rows 0..r's cells (a, b)
+    uint32_t *status;             // sticky status word (ST_*), or null
 };
 
 // host: the per-row masks of Params::sb_rows (boards of <= 128 cells)
@@ -105,6 +119,7 @@ inline Params make_params(int R, int C, int k, int smask, int num_moves, const u
     for (int w = 0; w < 2; w++) P.sb_nl[w] = P.sb_nf[w] = P.sb_h[w] = P.sb_in[w] = P.sb_u[w] = P.sb_v[w] = 0;
     P.sb_z = 0;
     P.sb_rows = nullptr;
+    P.status = nullptr;
     if (P.N <= 128) {
         for (int p = 0; p < P.N; p++) {
             const int c = p % C, w = p & 1, b = p >> 1;
@@ -357,7 +372,7 @@ __device__ __forceinline__ void draw_colours(const Params &P, int lane, const La
 }
 
 // --------------------------------------------------------------- board helpers
-__device__ __forceinline__ void action_coords(int R, int C, int a, int &r1, int &c1, int &r2, int &c2) {  // board.py:77-93
+__host__ __device__ __forceinline__ void action_coords(int R, int C, int a, int &r1, int &c1, int &r2, int &c2) {  // board.py:77-93
     if (a < C * (R - 1)) { r1 = a / C; c1 = a % C; r2 = r1 + 1; c2 = c1; }
     else { int i = a - C * (R - 1); r1 = i / (C - 1); c1 = i % (C - 1); r2 = r1; c2 = c1 + 1; }
 }
@@ -733,12 +748,14 @@ __device__ __forceinline__ void shuffle(const Params &P, WS &w, int lane, Rng &g
 
 // generate_board's / move's "while not possible_move() or lines" loop
 // (board.py:102-109, 381-391, remove_colour_lines :120-131).  Leaves the final
-// board's effective mask in w.effw.  Returns true when a shuffle ran.
+// board's effective mask in w.effw.  Returns FL_SHUF when a shuffle ran, FL_ERR
+// when a safety cap ended the loop.
 template <class WS>
-__device__ __forceinline__ bool ensure_playable(const Params &P, WS &w, int lane, const LaneJump &J, Rng &g,
+__device__ __forceinline__ int ensure_playable(const Params &P, WS &w, int lane, const LaneJump &J, Rng &g,
                                 const Cells<WS::NP> &cl) {
-    bool shuffled = false;
-    for (;;) {
+    int fl = 0;
+    int redraws = TMG_MAX_REDRAWS;
+    for (int shuffles = 0;; shuffles++) {
         // Redrawing rows 0..row leaves every cell an anchor test reads in rows
         // > row + 2 unchanged, so after it no anchor lies below max(row + 2, ra).
         int lim = P.R - 1;
@@ -746,28 +763,35 @@ __device__ __forceinline__ bool ensure_playable(const Params &P, WS &w, int lane
             int ra = 0;
             int r0 = first_line_row(P, w, lane, cl, lim, ra);
             if (r0 < 0) break;
+            if (--redraws < 0) return fl | FL_ERR;
             int row = P.R - 1 < r0 + 1 ? P.R - 1 : r0 + 1;   // colour plane only, rows 0..row
             draw_colours(P, lane, J, g, (row + 1) * P.C, w.brd, w.trash);
             WSYNC();
             lim = min(P.R - 1, max(row + 2, ra));
         }
         if (scan_effective(P, w, lane, cl, (P.smask & SP_COOKIE) == 0)) break;
+        if (shuffles >= TMG_MAX_SHUFFLES) return fl | FL_ERR;
         WSYNC();
         shuffle(P, w, lane, g);
-        shuffled = true;
+        fl = FL_SHUF;
     }
     WSYNC();
-    return shuffled;
+    return fl;
 }
 
-// generate_board, board.py:95-109
+// generate_board, board.py:95-109; returns FL_ERR when a safety cap was hit
 template <class WS>
-__device__ __forceinline__ void generate_board(const Params &P, WS &w, int lane, const LaneJump &J, Rng &g, const Cells<WS::NP> &cl) {
+__device__ __forceinline__ int generate_board(const Params &P, WS &w, int lane, const LaneJump &J, Rng &g, const Cells<WS::NP> &cl) {
     const int N = P.N;
     draw_colours(P, lane, J, g, N, w.brd, w.trash);
     for (int p = lane; p < N; p += 64) w.brd[N + p] = 1;
     WSYNC();
-    ensure_playable(P, w, lane, J, g, cl);
+    return ensure_playable(P, w, lane, J, g, cl) & FL_ERR;
+}
+
+// lane 0 ORs st into the sticky status word (a rare path: error / overflow)
+__device__ __forceinline__ void note_status(const Params &P, int lane, uint32_t st) {
+    if (st && lane == 0 && P.status) atomicOr(P.status, st);
 }
 
 template <class WS>
@@ -1349,7 +1373,7 @@ __device__ __forceinline__ int board_move(const Params &P, Ws<MAXN, GEN> &w, int
     elim += nn;                                                             // :378
     if (ovf) flags |= FL_OVF;
     if (err || w.sc[SC_ERR]) flags |= FL_ERR;
-    if (ensure_playable(P, w, lane, J, g, cl)) flags |= FL_SHUF;            // :381-391
+    flags |= ensure_playable(P, w, lane, J, g, cl);                         // :381-391
     STAMP(e, 3);
     return elim;
 }
@@ -1393,6 +1417,7 @@ __device__ __forceinline__ void step_env(
     const int t0 = __builtin_amdgcn_readfirstlane(timer[e]);
     if (t0 >= P.num_moves || a < 0 || a >= P.A) {                           // tile_match_env.py:94-95
         if (lane == 0) { reward[e] = 0; n_new[e] = 0; n_act[e] = 0; flags_out[e] = FL_ERR; }
+        note_status(P, lane, ST_CALLER);
         return;
     }
     int8_t *gb = board + e * 2 * N;
@@ -1422,6 +1447,7 @@ __device__ __forceinline__ void step_env(
         for (int p = lane; p < N; p += 64) ok &= w.brd[N + p] == 1;
         if (__ballot(!ok) != 0ULL) {
             if (lane == 0) { reward[e] = 0; n_new[e] = 0; n_act[e] = 0; flags_out[e] = FL_ERR; }
+            note_status(P, lane, ST_INTERNAL);
             return;
         }
     }
@@ -1444,8 +1470,8 @@ __device__ __forceinline__ void step_env(
     int tnew = t1;
     if (done && autoreset) {                                                // reset() without a seed
         if (autoreset == 1) {
-            if constexpr (SBNB > 0) sb_generate<SBNB, CODD>(P, w, lane, J, g, cl);
-            else generate_board(P, w, lane, J, g, cl);
+            if constexpr (SBNB > 0) flags |= sb_generate<SBNB, CODD>(P, w, lane, J, g, cl);
+            else flags |= generate_board(P, w, lane, J, g, cl);
             changed = true;
         }                                      // autoreset == 2: reset_kernel regenerates FL_RESET envs next
         tnew = 0;
@@ -1472,6 +1498,7 @@ __device__ __forceinline__ void step_env(
         n_act[e] = na;
         flags_out[e] = (uint8_t)flags;
     }
+    note_status(P, lane, ((flags & FL_ERR) ? ST_INTERNAL : 0u) | ((flags & FL_OVF) ? ST_OVERFLOW : 0u));
     STAMP(e, 7);
 }
 
@@ -1511,8 +1538,10 @@ __global__ __launch_bounds__(64 * TMG_WPB, MAXN > 128 ? TMG_RESET512_WAVES : 1) 
     Rng g = load_rng(rng + e * 5);
     const LaneJump J = load_jump(P, lane, g);
     const Cells<MAXN / 64> cl = make_cells<MAXN / 64>(P, lane);
-    if constexpr (SBNB > 0) sb_generate<SBNB, CODD>(P, w, lane, J, g, cl);   // board.py:95-109
-    else generate_board(P, w, lane, J, g, cl);
+    int fl;
+    if constexpr (SBNB > 0) fl = sb_generate<SBNB, CODD>(P, w, lane, J, g, cl);   // board.py:95-109
+    else fl = generate_board(P, w, lane, J, g, cl);
+    note_status(P, lane, fl ? ST_INTERNAL : 0u);
     store_board(P, w, lane, board + e * 2 * N);
     store_rng(rng + e * 5, g, lane);
     for (int i = lane; i < W; i += 64) eff[e * W + i] = w.effw[i];

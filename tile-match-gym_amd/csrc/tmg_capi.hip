@@ -5,6 +5,8 @@
 #include <cstdlib>
 #include <cstring>
 #include <string>
+#include <utility>
+#include <vector>
 
 #include "tmg.h"
 #include "tmg_board.hip"
@@ -31,6 +33,7 @@ struct tmg_ctx {
     tmg::Params P;
     uint64_t *d_jump;
     uint64_t *d_sbrows;
+    uint32_t *d_status;  // sticky status word (tmg_status)
     int maxn;
     int sb;          // scalar-bitboard kernels usable (<= 128 cells, C <= 63); TMG_SB=0 disables (A/B)
     int defer_general;   // 128-cell general kernel: autoreset by a masked reset launch (TMG_DEFER=0 disables)
@@ -173,16 +176,92 @@ static int check_call(tmg_ctx *ctx, int64_t n) {
     return set_device(ctx);
 }
 
+// ---------------------------------------------------------------- viability
+// The reference's generate_board / move loop "while not possible_move() or
+// lines" (board.py:102-109, 381-391) never ends on a shape where no board is
+// both line-free and playable (e.g. 2x2, or one colour); on the device that
+// would be a wave that never retires.  tmg_create therefore asks for one such
+// board first.  All-normal boards: a line is 3 equal colours in a row or
+// column (board.py:158-193), an effective move a swap that makes one
+// (is_move_effective, board.py:735-787).
+namespace {
+
+bool has_line(const int *b, int R, int C) {
+    for (int r = 0; r < R; r++)
+        for (int c = 0; c < C; c++) {
+            const int x = b[r * C + c];
+            if (c + 2 < C && b[r * C + c + 1] == x && b[r * C + c + 2] == x) return true;
+            if (r + 2 < R && b[(r + 1) * C + c] == x && b[(r + 2) * C + c] == x) return true;
+        }
+    return false;
+}
+
+bool playable(int *b, int R, int C) {                 // possible_move on a line-free board
+    for (int a = 0; a < 2 * R * C - R - C; a++) {
+        int r1, c1, r2, c2;
+        tmg::action_coords(R, C, a, r1, c1, r2, c2);
+        const int p = r1 * C + c1, q = r2 * C + c2;
+        if (b[p] == b[q]) continue;
+        std::swap(b[p], b[q]);
+        const bool l = has_line(b, R, C);
+        std::swap(b[p], b[q]);
+        if (l) return true;
+    }
+    return false;
+}
+
+// Whether some R x C board with colours < k is line-free and playable:
+// exhaustively when there are at most 2^21 colourings, else by building
+// random line-free boards (row-major, a colour that completes no triple).
+bool shape_viable(int R, int C, int k) {
+    if (k < 2 || (R < 3 && C < 3)) return false;
+    const int N = R * C;
+    std::vector<int> b(N, 0);
+    double total = 1.0;
+    for (int i = 0; i < N; i++) total *= k;
+    if (total <= (double)(1 << 21)) {
+        for (;;) {
+            if (!has_line(b.data(), R, C) && playable(b.data(), R, C)) return true;
+            int i = N - 1;                            // odometer
+            while (i >= 0 && ++b[i] == k) b[i--] = 0;
+            if (i < 0) return false;
+        }
+    }
+    uint64_t x = 0x9E3779B97F4A7C15ULL;
+    auto rnd = [&x]() { x ^= x << 13; x ^= x >> 7; x ^= x << 17; return x; };
+    for (int attempt = 0; attempt < 4096; attempt++) {
+        bool ok = true;
+        for (int p = 0; p < N && ok; p++) {
+            const int r = p / C, c = p - r * C;
+            int choices[16], nc = 0;
+            for (int v = 0; v < k && v < 16; v++) {
+                if (c >= 2 && b[p - 1] == v && b[p - 2] == v) continue;
+                if (r >= 2 && b[p - C] == v && b[p - 2 * C] == v) continue;
+                choices[nc++] = v;
+            }
+            if (nc == 0) ok = false;
+            else b[p] = choices[rnd() % nc];
+        }
+        if (ok && playable(b.data(), R, C)) return true;
+    }
+    return false;
+}
+
+}  // namespace
+
 extern "C" {
 
 int tmg_create(tmg_ctx **out, int device, int rows, int cols, int colours, uint32_t specials_mask, int num_moves) {
     if (!out) return fail(-1, "null output pointer");
     *out = nullptr;
-    if (rows < 2 || cols < 2) return fail(-2, "board must be at least 2x2");
+    if (rows < 1 || cols < 1) return fail(-2, "board must be at least 1x1");
     if (rows > 64 || cols > 64 || rows * cols > 512) return fail(-2, "board too large (R,C <= 64, R*C <= 512)");
     if (colours < 1 || colours > 15) return fail(-2, "num_colours must be in [1, 15]");
     if (specials_mask > 15u) return fail(-2, "bad specials mask");
     if (num_moves < 1) return fail(-2, "num_moves must be >= 1");
+    if (!shape_viable(rows, cols, colours))
+        return fail(-2, "no playable board exists for this shape and colour count (the reference's "
+                        "generate_board would loop forever, board.py:102-109)");
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return fail(-3, "no HIP device available");
     if (device < 0 || device >= ndev) return fail(-3, "bad device index");
@@ -205,6 +284,16 @@ int tmg_create(tmg_ctx **out, int device, int rows, int cols, int colours, uint3
     if (rc) { (void)hipFree(c->d_jump); delete c; return rc; }
     P.jump = c->d_jump;
     c->d_sbrows = nullptr;
+    c->d_status = nullptr;
+    rc = hip_check(hipMalloc(&c->d_status, 16), "hipMalloc");
+    if (!rc) rc = hip_check(hipMemset(c->d_status, 0, 16), "hipMemset");
+    if (rc) {
+        (void)hipFree(c->d_jump);
+        if (c->d_status) (void)hipFree(c->d_status);
+        delete c;
+        return rc;
+    }
+    P.status = c->d_status;
     if (P.N <= 128) {
         uint64_t rows[64 * 4];
         tmg::build_sb_rows(P.R, P.C, rows);
@@ -212,6 +301,7 @@ int tmg_create(tmg_ctx **out, int device, int rows, int cols, int colours, uint3
         if (!rc) rc = hip_check(hipMemcpy(c->d_sbrows, rows, sizeof rows, hipMemcpyHostToDevice), "hipMemcpy");
         if (rc) {
             (void)hipFree(c->d_jump);
+            (void)hipFree(c->d_status);
             if (c->d_sbrows) (void)hipFree(c->d_sbrows);
             delete c;
             return rc;
@@ -225,9 +315,25 @@ int tmg_create(tmg_ctx **out, int device, int rows, int cols, int colours, uint3
 int tmg_destroy(tmg_ctx *ctx) {
     if (!ctx) return 0;
     (void)hipFree(ctx->d_jump);
+    (void)hipFree(ctx->d_status);
     if (ctx->d_sbrows) (void)hipFree(ctx->d_sbrows);
     delete ctx;
     return 0;
+}
+
+int tmg_status(tmg_ctx *ctx, uint32_t *status, int clear) {
+    if (!status) return fail(-1, "null output pointer");
+    int rc = check_call(ctx, 0);
+    if (rc) return rc;
+    rc = hip_check(hipDeviceSynchronize(), "hipDeviceSynchronize");
+    if (!rc) rc = hip_check(hipMemcpy(status, ctx->d_status, sizeof(uint32_t), hipMemcpyDeviceToHost), "hipMemcpy");
+    if (!rc && clear) rc = hip_check(hipMemset(ctx->d_status, 0, sizeof(uint32_t)), "hipMemset");
+    return rc;
+}
+
+int tmg_viable(int rows, int cols, int colours) {
+    if (rows < 1 || cols < 1 || rows > 64 || cols > 64 || rows * cols > 512 || colours < 1 || colours > 15) return 0;
+    return shape_viable(rows, cols, colours) ? 1 : 0;
 }
 
 int tmg_reset(tmg_ctx *ctx, int64_t n, int8_t *board, uint64_t *rng, int32_t *timer, uint64_t *eff,
@@ -360,6 +466,6 @@ __attribute__((visibility("default"))) int tmg_debug_stamps(uint64_t *host, int6
 int tmg_num_actions(const tmg_ctx *ctx) { return ctx ? ctx->P.A : -1; }
 int tmg_mask_words(const tmg_ctx *ctx) { return ctx ? ctx->P.W : -1; }
 const char *tmg_last_error(void) { return g_err.c_str(); }
-int tmg_abi_version(void) { return 1; }
+int tmg_abi_version(void) { return 2; }
 
 }  // extern "C"

@@ -371,14 +371,16 @@ __device__ __forceinline__ void sb_draw_rows(const Params &P, WS &w, int lane, c
 // "while not possible_move() or lines" (board.py:102-109, 381-391) on the
 // bitboards.  The LDS board is brought in sync before the effective-action
 // scan (whose mask it leaves in w.effw) and the shuffle.  `dirty`: c is newer
-// than the LDS board; `clean`: the board is known to hold no line.
+// than the LDS board; `clean`: the board is known to hold no line.  Returns
+// FL_SHUF when a shuffle ran, FL_ERR when a safety cap ended the loop.
 template <int NB, bool CODD, class WS>
-__device__ __forceinline__ bool sb_ensure(const Params &P, WS &w, int lane, const LaneJump &J, Rng &g,
-                                          const Cells<WS::NP> &cl, SBC &c, bool dirty, bool clean) {
+__device__ __forceinline__ int sb_ensure(const Params &P, WS &w, int lane, const LaneJump &J, Rng &g,
+                                         const Cells<WS::NP> &cl, SBC &c, bool dirty, bool clean) {
     int keyA, keyB;
     sb_line_keys(P, lane, keyA, keyB);
-    bool shuffled = false;
-    for (;;) {
+    int fl = 0;
+    int redraws = TMG_MAX_REDRAWS;
+    for (int shuffles = 0;; shuffles++) {
         if (!clean) {
             for (;;) {
                 const SBDrawPre pre = sb_draw_pre(J, g);
@@ -387,6 +389,7 @@ __device__ __forceinline__ bool sb_ensure(const Params &P, WS &w, int lane, cons
                 // keep the jump-ahead above the exit test (else it is sunk below it)
                 TMG_KEEP_V3(pre.sj.lo, pre.sj.hi, pre.out);
                 if (key < 0) break;
+                if (--redraws < 0) { fl |= FL_ERR; break; }
                 const int r0 = sb_line_row_of_key<CODD>(P, d, key);
                 const int row = P.R - 1 < r0 + 1 ? P.R - 1 : r0 + 1;   // colour plane only, rows 0..row
                 sb_draw_rows<NB>(P, w, lane, J, g, row, c, pre);
@@ -399,25 +402,28 @@ __device__ __forceinline__ bool sb_ensure(const Params &P, WS &w, int lane, cons
             WSYNC();
             dirty = false;
         }
+        if (fl & FL_ERR) break;
         if (scan_effective_clean<false>(P, w, lane)) break;   // types all 1, no line
+        if (shuffles >= TMG_MAX_SHUFFLES) { fl |= FL_ERR; break; }
         WSYNC();
         shuffle(P, w, lane, g);
         c = sb_codes_from_lds(P, w.brd, lane);
-        shuffled = true;
+        fl |= FL_SHUF;
         clean = false;
     }
     WSYNC();
-    return shuffled;
+    return fl;
 }
 
-// generate_board, board.py:95-109 (types all 1; colours from the env stream)
+// generate_board, board.py:95-109 (types all 1; colours from the env stream);
+// returns FL_ERR when a safety cap was hit
 template <int NB, bool CODD, class WS>
-__device__ __forceinline__ void sb_generate(const Params &P, WS &w, int lane, const LaneJump &J, Rng &g,
-                                            const Cells<WS::NP> &cl) {
+__device__ __forceinline__ int sb_generate(const Params &P, WS &w, int lane, const LaneJump &J, Rng &g,
+                                           const Cells<WS::NP> &cl) {
     SBC c{0, 0};
     sb_draw_rows<NB>(P, w, lane, J, g, P.R - 1, c, sb_draw_pre(J, g));
     for (int p = lane; p < P.N; p += 64) w.brd[P.N + p] = 1;
-    sb_ensure<NB, CODD>(P, w, lane, J, g, cl, c, true, false);
+    return sb_ensure<NB, CODD>(P, w, lane, J, g, cl, c, true, false) & FL_ERR;
 }
 
 // Board.move, board.py:330-395, for a board that can hold no special (every
@@ -445,7 +451,7 @@ __device__ __forceinline__ int sb_move(const Params &P, WS &w, int lane, const L
         sb_gravity_refill<CODD>(P, w, lane, J, g, clr, tot, c);
     }
     STAMP(e, 2);
-    if (sb_ensure<NB, CODD>(P, w, lane, J, g, cl, c, false, true)) flags |= FL_SHUF;   // :381-391
+    flags |= sb_ensure<NB, CODD>(P, w, lane, J, g, cl, c, false, true);   // :381-391
     STAMP(e, 3);
     return elim;
 }

@@ -14,9 +14,11 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("TMG_LIB") or os.path.join(_HERE, "_lib", "libtmg.so")   # TMG_LIB: A/B another build
 EXPORTS = ("tmg_create", "tmg_destroy", "tmg_reset", "tmg_step", "tmg_effective",
            "tmg_num_actions", "tmg_mask_words", "tmg_last_error", "tmg_abi_version",
-           "tmg_onehot", "tmg_onehot_channels", "tmg_count_states", "tmg_sample_effective")
+           "tmg_onehot", "tmg_onehot_channels", "tmg_count_states", "tmg_sample_effective", "tmg_status",
+           "tmg_viable")
 DTYPE_F32, DTYPE_U8, DTYPE_I32 = 0, 1, 2
-ABI_VERSION = 1
+ABI_VERSION = 2
+STATUS_INTERNAL, STATUS_OVERFLOW, STATUS_CALLER = 1, 2, 4
 
 SPECIAL_BITS = {"cookie": 1, "vertical_laser": 2, "horizontal_laser": 4, "bomb": 8}
 FLAG_DONE, FLAG_COMBO, FLAG_SHUFFLED, FLAG_RESET, FLAG_OVERFLOW, FLAG_ERROR = 1, 2, 4, 8, 0x40, 0x80
@@ -55,9 +57,11 @@ def load():
     L.tmg_onehot_channels.argtypes = [P]
     L.tmg_count_states.argtypes = [I, I, I, I, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64)]
     L.tmg_sample_effective.argtypes = [P, I64, P, ctypes.c_uint64, I64, ctypes.c_int32, P, P]
+    L.tmg_status.argtypes = [P, ctypes.POINTER(ctypes.c_uint32), I]
+    L.tmg_viable.argtypes = [I, I, I]
     for name in ("tmg_create", "tmg_destroy", "tmg_reset", "tmg_step", "tmg_effective",
                  "tmg_num_actions", "tmg_mask_words", "tmg_abi_version", "tmg_onehot", "tmg_onehot_channels",
-                 "tmg_sample_effective",
+                 "tmg_sample_effective", "tmg_status", "tmg_viable",
                  "tmg_count_states"):
         getattr(L, name).restype = I
     if L.tmg_abi_version() != ABI_VERSION:
@@ -115,6 +119,12 @@ class Context:
         check(load().tmg_step(self._h, int(n), board, rng, timer, actions, reward, n_new, n_act, flags, eff,
                               int(trust_eff), int(autoreset), stream))
 
+    def status(self, clear: bool = False) -> int:
+        """Sticky STATUS_* bits of this context (waits for the device)."""
+        v = ctypes.c_uint32(0)
+        check(load().tmg_status(self._h, ctypes.byref(v), int(clear)))
+        return int(v.value)
+
     def effective(self, n, board, eff, stream):
         check(load().tmg_effective(self._h, int(n), board, eff, stream))
 
@@ -127,6 +137,11 @@ class Context:
     def sample_effective(self, n, eff, key, first_env, t, actions, stream):
         check(load().tmg_sample_effective(self._h, int(n), eff, int(key) & 0xFFFFFFFFFFFFFFFF, int(first_env),
                                           int(t), actions, stream))
+
+
+def viable(rows: int, cols: int, colours: int) -> bool:
+    """Whether a line-free playable board exists (tmg_viable; tmg_create refuses the others)."""
+    return bool(load().tmg_viable(int(rows), int(cols), int(colours)))
 
 
 def count_states(device_index: int, rows: int, cols: int, colours: int):

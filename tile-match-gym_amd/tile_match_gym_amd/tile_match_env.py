@@ -183,8 +183,9 @@ class TileMatchEnv(_EnvBase):
         self._download()
         o = out[:, 0].cpu().numpy()
         flags = int(self._d_flags[0].item())
-        if flags & _native.FLAG_ERROR:
-            raise _native.TmgError("device reported an error for this move")
+        if flags & (_native.FLAG_ERROR | _native.FLAG_OVERFLOW):
+            raise _native.TmgError(f"device reported {'an error' if flags & _native.FLAG_ERROR else 'an overflow'} "
+                                   "for this move")
         num_eliminations, num_new_specials, num_specials_activated = int(o[0]), int(o[1]), int(o[2])
         self.timer += 1
         done = self.timer == self.num_moves

@@ -109,8 +109,26 @@ class TileMatchVecEnv:
 
     def set_seed(self, seeds):
         """Re-seed every env (== tile_match_env.py:79-82 per env)."""
+        self.join()
         w = batch_rng_words(seeds)
         self.rng.copy_(torch.from_numpy(w.view(np.int64)))
+
+    def stagger_phases(self, first_env: int = 0):
+        """Set env i's timer to (first_env + i) mod num_moves, right after a
+        reset.  Same state as env i having played that many ineffective moves
+        (board.py:352-353: no board or RNG change, tile_match_env.py:100 counts
+        the move), so each later step finishes ~N/num_moves episodes instead of
+        all N every num_moves-th step.  Pass the shard's global offset as
+        first_env to keep the layout shard-invariant."""
+        self.join()
+        g = torch.arange(first_env, first_env + self.num_envs, device=self.device, dtype=torch.int64)
+        self.timer.copy_((g % self.num_moves).to(torch.int32))
+
+    def status(self, clear: bool = False) -> int:
+        """Sticky _native.STATUS_* bits: OR over every env of every step since
+        the last clear (waits for the device)."""
+        self.join()
+        return self.ctx.status(clear)
 
     def _fork(self):
         """Group streams wait for the work already queued on the current stream."""
@@ -159,6 +177,7 @@ class TileMatchVecEnv:
             "shuffled": (flags & _native.FLAG_SHUFFLED) != 0,
             "effective_bits": self.eff,
             "error": (flags & _native.FLAG_ERROR) != 0,
+            "overflow": (flags & _native.FLAG_OVERFLOW) != 0,
         }
         done = (flags & _native.FLAG_DONE) != 0
         return self._obs(), self.reward, done, torch.zeros_like(done), info
@@ -218,6 +237,7 @@ class TileMatchVecEnv:
 
     def effective_mask(self) -> torch.Tensor:
         """(N, A) bool mask of effective actions, unpacked from the bitmask."""
+        self.join()
         bits = torch.arange(64, device=self.device, dtype=torch.int64)
         m = ((self.eff.unsqueeze(-1) >> bits) & 1).reshape(self.num_envs, -1)[:, :self.num_actions]
         return m.bool()

@@ -55,8 +55,8 @@ class TileMatchVectorEnv:
         self.num_moves = num_moves
         R, C = num_rows, num_cols
         nsp = len(colour_specials)
-        # tile_match_env.py:62-77 (incl. the type plane's high = num_colour_specials + 2)
-        low = np.array([np.zeros((R, C), np.int32), np.full((R, C), -1, np.int32)])
+        # tile_match_env.py:52-77 (type plane: low = -num_colourless_specials, high = num_colour_specials + 2)
+        low = np.array([np.zeros((R, C), np.int32), np.full((R, C), -len(colourless_specials), np.int32)])
         high = np.array([np.full((R, C), num_colours, np.int32), np.full((R, C), nsp + 2, np.int32)])
         self.single_observation_space = Dict({"board": Box(low=low, high=high, shape=(2, R, C), dtype=np.int32),
                                               "num_moves_left": Discrete(num_moves + 1)})
@@ -129,6 +129,8 @@ class TileMatchVectorEnv:
         infos["num_new_specials"] = torch.where(live, v.n_new, zero_i)
         infos["num_specials_activated"] = torch.where(live, v.n_act, zero_i)
         infos["shuffled"] = ((flags & _native.FLAG_SHUFFLED) != 0) & live
+        # a live env whose step met an internal error / capacity overflow (never expected)
+        infos["error"] = ((flags & (_native.FLAG_ERROR | _native.FLAG_OVERFLOW)) != 0) & live
         if self.action_masks:
             infos["action_mask"] = self._mask()
         trunc = torch.zeros_like(term)

@@ -56,6 +56,7 @@ inline unsigned min(unsigned a, unsigned b) { return a < b ? a : b; }
 inline unsigned max(unsigned a, unsigned b) { return a > b ? a : b; }
 
 inline uint64_t __builtin_amdgcn_s_memrealtime() { return 0; }
+inline unsigned atomicOr(unsigned *p, unsigned v) { unsigned o = *p; *p |= v; return o; }
 
 #define TMG_CONST_AS
 #define TMG_KEEP_V3(x, y, z) ((void)0)
