@@ -8,11 +8,17 @@ per env group; `--groups` groups run on separate HIP streams so one group's
 launch tail overlaps the next group's launch — same boards, same work),
 uniform random actions pre-staged in HBM, autoreset on (num_moves = 30).
 
-Episode phases are staggered after the reset (`TileMatchVecEnv.stagger_phases`:
-env i starts at timer (global i) mod 30, the state of i mod 30 ineffective
-moves), so every step of any timed window finishes ~1/30 of the episodes and
-regenerates those boards (tile_match_env.py:84-91 -> board.py:95-131): the
-amortised work of the aligned run, whatever --steps / --warmup are.
+Episode phases (`--phase-blocks P`, default 3 = the env groups): after the
+reset the shard's envs form P contiguous blocks whose episodes are offset by
+30/P steps (`TileMatchVecEnv.stagger_phases`: a timer of m is the state after
+m ineffective moves).  Every 10 steps one block's episodes end and its boards
+are regenerated (tile_match_env.py:84-91 -> board.py:95-131), so any timed
+window of a multiple of 10 steps (the driver's 20, the default 300) holds
+exactly its share of the reset work (20 steps: 2/3 of the boards), and each
+block's regeneration overlaps the other groups' steps on their streams.
+P = 1 is the aligned run (every env resets on the same step); P = 0 staggers
+every env (env i at timer i mod 30: each step regenerates N/30 boards, and the
+step time is then the slowest of those regenerations).
 
 Multi-GPU: one process per GPU, each stepping its own contiguous shard of envs
 (seed = global env index); there is no collective on the data path, only a
@@ -84,7 +90,7 @@ def _time_oracle(R, C, k, smask, moves, n, threads, budget_s, policy):
     A = 2 * R * C - R - C
     o = orc.OracleBatch(R, C, k, smask, moves, batch_rng_words(range(n)), threads=threads)
     o.reset()
-    o.timer[:] = np.arange(n) % moves              # the bench's staggered phases
+    o.timer[:] = np.arange(n) % moves              # staggered phases: the amortised reset share every step
     T = 300
     acts = synthetic_actions(range(n), T, A)
     steps = 0
@@ -163,7 +169,9 @@ def main():
     ap.add_argument("--policy", default="uniform", choices=("uniform", "effective"),
                     help="uniform: random actions over all A (headline); effective: every env samples uniformly "
                          "from its effective actions on device each step (SURVEY §8(d) secondary mode)")
-    ap.add_argument("--no-stagger", action="store_true", help="aligned episodes (every env resets on the same step)")
+    ap.add_argument("--phase-blocks", type=int, default=3,
+                    help="episode phase blocks: P contiguous env blocks offset by 30/P steps (1 = aligned, "
+                         "0 = every env staggered)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--dry-run", action="store_true", help="print each rank's shard layout and exit (no GPU)")
     args = ap.parse_args()
@@ -200,8 +208,8 @@ def main():
     T = 300
     acts = torch.from_numpy(synthetic_actions(rng_, T, A)).to(dev)
     env.reset()
-    if not args.no_stagger:
-        env.stagger_phases(first_env=rng_.start)
+    if args.phase_blocks != 1:
+        env.stagger_phases(blocks=args.phase_blocks, first_env=rng_.start)
     env.status(clear=True)
 
     def step(t):
@@ -282,7 +290,10 @@ def main():
                      "synthetic (each step every env samples uniformly from its effective actions on device, "
                      "counter-based per (step, global env); seeds = global env index)"),
             "config": {"workload": f"{args.config}: {desc}, num_moves=30, autoreset"
-                                   + ("" if args.no_stagger else ", episode phases staggered (timer0 = env mod 30)")
+                                   + (", episodes aligned" if args.phase_blocks == 1 else
+                                      ", every env's episode phase staggered (timer0 = env mod 30)" if args.phase_blocks <= 0
+                                      else f", {args.phase_blocks} episode-phase blocks offset by "
+                                           f"{moves // args.phase_blocks} steps")
                                    + ("" if args.policy == "uniform" else ", effective-action policy"),
                        "boards_per_gpu": nb, "rows": R, "cols": C, "colours": k,
                        "specials": cl + co, "env_groups_per_gpu": env.groups,

@@ -210,3 +210,40 @@ def test_env_groups_match_single_stream(R, C, k, sm):
     torch.cuda.synchronize()
     for f in ("board", "rng", "timer", "eff", "reward", "n_new", "n_act", "flags"):
         assert torch.equal(getattr(e1, f), getattr(e3, f)), f
+
+
+@pytest.mark.parametrize("blocks", [0, 3])
+@pytest.mark.parametrize("R,C,k,sm", [(10, 10, 4, 0), (10, 10, 4, 14)])
+def test_bench_phase_stagger_vs_oracle(blocks, R, C, k, sm):
+    """The bench's workload: episode phases offset after the reset
+    (stagger_phases; blocks=3 with 3 env groups, blocks=0 every env), the
+    synthetic action stream, autoreset — vs the oracle given the same timers."""
+    from tile_match_gym_amd.shard import synthetic_actions
+    from tile_match_gym_amd.vec_env import TileMatchVecEnv
+    co = [nm for b, nm in ((8, "bomb"), (2, "vertical_laser"), (4, "horizontal_laser")) if sm & b]
+    n = 3000
+    env = TileMatchVecEnv(n, R, C, k, 30, [], co, seed=5, device=DEV, groups=3)
+    ref = orc.OracleBatch(R, C, k, sm, 30, env.rng_words().copy(), threads=16)
+    env.reset()
+    ref.reset()
+    env.stagger_phases(blocks=blocks)
+    t0 = env.timer.cpu().numpy()
+    if blocks:
+        assert sorted(set(t0.tolist())) == [0, 10, 20]
+        assert (t0[:1000] == 0).all() and (t0[1000:2000] == 10).all() and (t0[2000:] == 20).all()
+    else:
+        assert np.array_equal(t0, np.arange(n) % 30)
+    ref.timer[:] = t0
+    acts = synthetic_actions(range(n), 45, env.num_actions)
+    dacts = torch.from_numpy(acts).to(DEV)
+    for t in range(45):
+        env.step_raw(dacts[t])
+        ref.step(acts[t], autoreset=True)
+        env.join()
+        f = env.flags.cpu().numpy()
+        assert np.array_equal(f, ref.flags), f"step {t}: flags"
+        assert np.array_equal(env.board.cpu().numpy(), ref.board), f"step {t}: board"
+        assert np.array_equal(env.reward.cpu().numpy(), ref.reward), f"step {t}: reward"
+    assert np.array_equal(env.rng_words(), ref.rng)
+    assert np.array_equal(env.timer.cpu().numpy(), ref.timer)
+    assert env.status() == 0

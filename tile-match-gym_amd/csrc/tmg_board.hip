@@ -47,6 +47,9 @@ namespace tmg {
 #define TMG_XCD 1          // XCD-aware workgroup -> env mapping
 #endif
 
+#ifndef TMG_STATUS
+#define TMG_STATUS 1           // 0: no sticky status word (A/B of its cost only; tmg_status then reads 0)
+#endif
 #ifndef TMG_RESET512_WAVES
 #define TMG_RESET512_WAVES 4   // min waves per SIMD for the 512-cell reset kernel (caps its VGPRs)
 #endif
@@ -63,16 +66,16 @@ namespace tmg {
 enum : int { SP_COOKIE = 1, SP_VLASER = 2, SP_HLASER = 4, SP_BOMB = 8 };
 enum : int { M_NORMAL = 0, M_VLASER = 1, M_HLASER = 2, M_BOMB = 3, M_COOKIE = 4 };
 enum : int { FL_DONE = 1, FL_COMBO = 2, FL_SHUF = 4, FL_RESET = 8, FL_OVF = 0x40, FL_ERR = 0x80 };
-// sticky status word (tmg_status): OR of what any env met since the last clear
+// sticky status (tmg_status): what any env met since the last clear
 enum : uint32_t { ST_INTERNAL = 1, ST_OVERFLOW = 2, ST_CALLER = 4 };
 
-// Safety caps of the "while not possible_move() or lines" loop (board.py:102-109,
-// 381-391).  tmg_create rejects shapes on which no playable board exists, so a
-// real board never comes near them; reaching one ends the loop with FL_ERR
-// instead of spinning the wave forever (the reference would spin).
-#ifndef TMG_MAX_REDRAWS
-#define TMG_MAX_REDRAWS (1 << 20)    // remove_colour_lines calls per loop
-#endif
+// Safety cap of the "while not possible_move() or lines" loop (board.py:102-109,
+// 381-391).  Its redraw part ends with probability 1 on every shape tmg_create
+// accepts (a full redraw, row R-1, can always come out line-free, and every
+// line found lets the next redraw reach its rows), so it is not counted.  The
+// shuffle part can spin forever on a colour multiset that has no playable
+// line-free arrangement (e.g. 3x3 with at most two tiles of each colour): there
+// the reference loops forever; here the wave ends the loop with FL_ERR.
 #ifndef TMG_MAX_SHUFFLES
 #define TMG_MAX_SHUFFLES (1 << 12)   // shuffles per loop
 #endif
@@ -90,7 +93,7 @@ struct Params {
     uint64_t sb_z;                // one column's cells of one word, from bit 0
     uint64_t sb_in[2], sb_u[2], sb_v[2];   // cells of the board / of rows >= 1 / of rows >= 2
     const uint64_t *sb_rows;      // [R][4]: row r's cells (a, b), rows 0..r's cells (a, b)
-    uint32_t *status;             // sticky status word (ST_*), or null
+    uint32_t *status;             // sticky status words, one per ST_* bit
 };
 
 // host: the per-row masks of Params::sb_rows (boards of <= 128 cells)
@@ -749,12 +752,11 @@ __device__ __forceinline__ void shuffle(const Params &P, WS &w, int lane, Rng &g
 // generate_board's / move's "while not possible_move() or lines" loop
 // (board.py:102-109, 381-391, remove_colour_lines :120-131).  Leaves the final
 // board's effective mask in w.effw.  Returns FL_SHUF when a shuffle ran, FL_ERR
-// when a safety cap ended the loop.
+// when the shuffle cap ended the loop.
 template <class WS>
 __device__ __forceinline__ int ensure_playable(const Params &P, WS &w, int lane, const LaneJump &J, Rng &g,
                                 const Cells<WS::NP> &cl) {
     int fl = 0;
-    int redraws = TMG_MAX_REDRAWS;
     for (int shuffles = 0;; shuffles++) {
         // Redrawing rows 0..row leaves every cell an anchor test reads in rows
         // > row + 2 unchanged, so after it no anchor lies below max(row + 2, ra).
@@ -763,7 +765,6 @@ __device__ __forceinline__ int ensure_playable(const Params &P, WS &w, int lane,
             int ra = 0;
             int r0 = first_line_row(P, w, lane, cl, lim, ra);
             if (r0 < 0) break;
-            if (--redraws < 0) return fl | FL_ERR;
             int row = P.R - 1 < r0 + 1 ? P.R - 1 : r0 + 1;   // colour plane only, rows 0..row
             draw_colours(P, lane, J, g, (row + 1) * P.C, w.brd, w.trash);
             WSYNC();
@@ -789,9 +790,18 @@ __device__ __forceinline__ int generate_board(const Params &P, WS &w, int lane, 
     return ensure_playable(P, w, lane, J, g, cl) & FL_ERR;
 }
 
-// lane 0 ORs st into the sticky status word (a rare path: error / overflow)
+// lane 0 records st in the sticky status words (a rare path: error / overflow)
 __device__ __forceinline__ void note_status(const Params &P, int lane, uint32_t st) {
-    if (st && lane == 0 && P.status) atomicOr(P.status, st);
+#if TMG_STATUS
+    // one word per status bit, each only ever set to 1: plain stores, no atomics
+    if (st && lane == 0) {
+        if (st & ST_INTERNAL) P.status[0] = 1u;
+        if (st & ST_OVERFLOW) P.status[1] = 1u;
+        if (st & ST_CALLER) P.status[2] = 1u;
+    }
+#else
+    (void)P; (void)lane; (void)st;
+#endif
 }
 
 template <class WS>
@@ -1404,9 +1414,10 @@ __device__ __forceinline__ void store_rng(uint64_t *p, const Rng &g, int lane) {
 // lean variant, board generation in both); CODD = C is odd.  autoreset: 1
 // regenerates a finished board here, 2 leaves it to a following reset_kernel
 // launch masked by FL_RESET (the 512-cell kernels: the reset kernel's
-// occupancy is far higher than the general step kernel's).
+// occupancy is far higher than the general step kernel's).  Returns the ST_*
+// bits this step raises for the sticky status word.
 template <int MAXN, bool GEN, int SBNB, bool CODD>
-__device__ __forceinline__ void step_env(
+__device__ __forceinline__ uint32_t step_env(
     const Params &P, Ws<MAXN, GEN> &w, int lane, int64_t e, int8_t *__restrict__ board, uint64_t *__restrict__ rng, int32_t *__restrict__ timer,
     const int32_t *__restrict__ actions, int32_t *__restrict__ reward, int32_t *__restrict__ n_new,
     int32_t *__restrict__ n_act, uint8_t *__restrict__ flags_out, uint64_t *__restrict__ eff, int trust_eff,
@@ -1417,8 +1428,7 @@ __device__ __forceinline__ void step_env(
     const int t0 = __builtin_amdgcn_readfirstlane(timer[e]);
     if (t0 >= P.num_moves || a < 0 || a >= P.A) {                           // tile_match_env.py:94-95
         if (lane == 0) { reward[e] = 0; n_new[e] = 0; n_act[e] = 0; flags_out[e] = FL_ERR; }
-        note_status(P, lane, ST_CALLER);
-        return;
+        return ST_CALLER;
     }
     int8_t *gb = board + e * 2 * N;
     uint64_t *ge = eff + e * W;
@@ -1431,7 +1441,7 @@ __device__ __forceinline__ void step_env(
         if (done) for (int i = lane; i < W; i += 64) ge[i] = 0ULL;          // tile_match_env.py:119-120
         if (lane == 0) { timer[e] = t1; reward[e] = 0; n_new[e] = 0; n_act[e] = 0; flags_out[e] = (uint8_t)flags; }
         STAMP(e, 7);
-        return;
+        return 0;
     }
     int r1, c1, r2, c2;
     action_coords(P.R, P.C, a, r1, c1, r2, c2);
@@ -1447,8 +1457,7 @@ __device__ __forceinline__ void step_env(
         for (int p = lane; p < N; p += 64) ok &= w.brd[N + p] == 1;
         if (__ballot(!ok) != 0ULL) {
             if (lane == 0) { reward[e] = 0; n_new[e] = 0; n_act[e] = 0; flags_out[e] = FL_ERR; }
-            note_status(P, lane, ST_INTERNAL);
-            return;
+            return ST_INTERNAL;
         }
     }
     if (!trust_eff) {
@@ -1498,8 +1507,8 @@ __device__ __forceinline__ void step_env(
         n_act[e] = na;
         flags_out[e] = (uint8_t)flags;
     }
-    note_status(P, lane, ((flags & FL_ERR) ? ST_INTERNAL : 0u) | ((flags & FL_OVF) ? ST_OVERFLOW : 0u));
     STAMP(e, 7);
+    return ((flags & FL_ERR) ? ST_INTERNAL : 0u) | ((flags & FL_OVF) ? ST_OVERFLOW : 0u);
 }
 
 // TileMatchEnv.step over a batch, one wave per env.
@@ -1516,8 +1525,9 @@ __global__ TMG_LAUNCH_BOUNDS void step_kernel(
     WS &w = reinterpret_cast<WS *>(smem)[wv];
     const int64_t e = wg_env0() + wv;
     if (e >= n) return;
-    step_env<MAXN, GEN, SBNB, CODD>(P, w, lane, e, board, rng, timer, actions, reward, n_new, n_act, flags_out, eff,
-                                    trust_eff, autoreset);
+    const uint32_t st = step_env<MAXN, GEN, SBNB, CODD>(P, w, lane, e, board, rng, timer, actions, reward, n_new,
+                                                        n_act, flags_out, eff, trust_eff, autoreset);
+    note_status(P, lane, st);
 }
 
 // TileMatchEnv.reset without a seed (tile_match_env.py:84-91)

@@ -33,7 +33,7 @@ struct tmg_ctx {
     tmg::Params P;
     uint64_t *d_jump;
     uint64_t *d_sbrows;
-    uint32_t *d_status;  // sticky status word (tmg_status)
+    uint32_t *d_status;  // sticky status words (tmg_status): one per TMG_STATUS_* bit
     int maxn;
     int sb;          // scalar-bitboard kernels usable (<= 128 cells, C <= 63); TMG_SB=0 disables (A/B)
     int defer_general;   // 128-cell general kernel: autoreset by a masked reset launch (TMG_DEFER=0 disables)
@@ -326,8 +326,12 @@ int tmg_status(tmg_ctx *ctx, uint32_t *status, int clear) {
     int rc = check_call(ctx, 0);
     if (rc) return rc;
     rc = hip_check(hipDeviceSynchronize(), "hipDeviceSynchronize");
-    if (!rc) rc = hip_check(hipMemcpy(status, ctx->d_status, sizeof(uint32_t), hipMemcpyDeviceToHost), "hipMemcpy");
-    if (!rc && clear) rc = hip_check(hipMemset(ctx->d_status, 0, sizeof(uint32_t)), "hipMemset");
+    uint32_t words[4] = {0, 0, 0, 0};      // one word per status bit (note_status in tmg_board.hip)
+    if (!rc) rc = hip_check(hipMemcpy(words, ctx->d_status, sizeof words, hipMemcpyDeviceToHost), "hipMemcpy");
+    if (rc) return rc;
+    *status = (words[0] ? TMG_STATUS_INTERNAL : 0u) | (words[1] ? TMG_STATUS_OVERFLOW : 0u) |
+              (words[2] ? TMG_STATUS_CALLER : 0u);
+    if (clear) rc = hip_check(hipMemset(ctx->d_status, 0, sizeof words), "hipMemset");
     return rc;
 }
 

@@ -372,14 +372,13 @@ __device__ __forceinline__ void sb_draw_rows(const Params &P, WS &w, int lane, c
 // bitboards.  The LDS board is brought in sync before the effective-action
 // scan (whose mask it leaves in w.effw) and the shuffle.  `dirty`: c is newer
 // than the LDS board; `clean`: the board is known to hold no line.  Returns
-// FL_SHUF when a shuffle ran, FL_ERR when a safety cap ended the loop.
+// FL_SHUF when a shuffle ran, FL_ERR when the shuffle cap ended the loop.
 template <int NB, bool CODD, class WS>
 __device__ __forceinline__ int sb_ensure(const Params &P, WS &w, int lane, const LaneJump &J, Rng &g,
                                          const Cells<WS::NP> &cl, SBC &c, bool dirty, bool clean) {
     int keyA, keyB;
     sb_line_keys(P, lane, keyA, keyB);
     int fl = 0;
-    int redraws = TMG_MAX_REDRAWS;
     for (int shuffles = 0;; shuffles++) {
         if (!clean) {
             for (;;) {
@@ -389,7 +388,6 @@ __device__ __forceinline__ int sb_ensure(const Params &P, WS &w, int lane, const
                 // keep the jump-ahead above the exit test (else it is sunk below it)
                 TMG_KEEP_V3(pre.sj.lo, pre.sj.hi, pre.out);
                 if (key < 0) break;
-                if (--redraws < 0) { fl |= FL_ERR; break; }
                 const int r0 = sb_line_row_of_key<CODD>(P, d, key);
                 const int row = P.R - 1 < r0 + 1 ? P.R - 1 : r0 + 1;   // colour plane only, rows 0..row
                 sb_draw_rows<NB>(P, w, lane, J, g, row, c, pre);
@@ -402,7 +400,6 @@ __device__ __forceinline__ int sb_ensure(const Params &P, WS &w, int lane, const
             WSYNC();
             dirty = false;
         }
-        if (fl & FL_ERR) break;
         if (scan_effective_clean<false>(P, w, lane)) break;   // types all 1, no line
         if (shuffles >= TMG_MAX_SHUFFLES) { fl |= FL_ERR; break; }
         WSYNC();

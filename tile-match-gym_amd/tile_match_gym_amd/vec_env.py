@@ -113,16 +113,29 @@ class TileMatchVecEnv:
         w = batch_rng_words(seeds)
         self.rng.copy_(torch.from_numpy(w.view(np.int64)))
 
-    def stagger_phases(self, first_env: int = 0):
-        """Set env i's timer to (first_env + i) mod num_moves, right after a
-        reset.  Same state as env i having played that many ineffective moves
-        (board.py:352-353: no board or RNG change, tile_match_env.py:100 counts
-        the move), so each later step finishes ~N/num_moves episodes instead of
-        all N every num_moves-th step.  Pass the shard's global offset as
-        first_env to keep the layout shard-invariant."""
+    def stagger_phases(self, blocks: int = 0, first_env: int = 0):
+        """Offset the episode phases right after a reset by setting timers.  A
+        timer of m is the state after m ineffective moves (board.py:352-353: no
+        board or RNG change; tile_match_env.py:100 counts the move).
+
+        blocks = 0: env i gets (first_env + i) mod num_moves, so every step
+        finishes ~N/num_moves episodes (pass the shard's global offset as
+        first_env to keep the layout shard-invariant).
+        blocks = P > 0: the envs are split into P contiguous blocks (the same
+        split as `groups` = P), block b starting at b * num_moves // P, so
+        every num_moves // P steps one block (N/P envs) finishes its episodes."""
         self.join()
-        g = torch.arange(first_env, first_env + self.num_envs, device=self.device, dtype=torch.int64)
-        self.timer.copy_((g % self.num_moves).to(torch.int32))
+        N, M = self.num_envs, self.num_moves
+        if blocks and blocks > 0:
+            P = min(int(blocks), N)
+            i = torch.arange(N, device=self.device, dtype=torch.int64)
+            b = torch.zeros(N, device=self.device, dtype=torch.int64)
+            for g in range(1, P):
+                b += (i >= g * N // P).to(torch.int64)
+            self.timer.copy_(((b * M) // P % M).to(torch.int32))
+        else:
+            g = torch.arange(first_env, first_env + N, device=self.device, dtype=torch.int64)
+            self.timer.copy_((g % M).to(torch.int32))
 
     def status(self, clear: bool = False) -> int:
         """Sticky _native.STATUS_* bits: OR over every env of every step since
