@@ -301,6 +301,7 @@ def main():
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 6),
                          "traffic": traffic.get("hbm_bytes_per_launch") if traffic else None,
+                         "traffic_bytes_per_env_step": traffic.get("hbm_bytes_per_env_step") if traffic else None,
                          "algorithmic_bytes_per_env_step": bpu, "device_ms_per_step": round(step_ms, 4),
                          "kernel_ms_per_launch": round(kern_ms, 4), "envs_per_launch": launch_envs,
                          "per_launch_gbs": round(bpu * launch_envs / (kern_ms * 1e-3) / 1e9, 2),

@@ -121,18 +121,26 @@ class TileMatchVecEnv:
         blocks = 0: env i gets (first_env + i) mod num_moves, so every step
         finishes ~N/num_moves episodes (pass the shard's global offset as
         first_env to keep the layout shard-invariant).
-        blocks = P > 0: the envs are split into P contiguous blocks (the same
-        split as `groups` = P), block b starting at b * num_moves // P, so
-        every num_moves // P steps one block (N/P envs) finishes its episodes."""
+        blocks = P > 0: each env group's range is split into Pg = ceil(P / groups)
+        contiguous sub-blocks; sub-block j of group g starts at phase
+        j * M / Pg + g * M / (Pg * groups) (M = num_moves, floors).  Every
+        group then finishes a sub-block's episodes every M / Pg steps, and the
+        groups take turns, so a window of a multiple of M / Pg steps holds the
+        same reset work on every group's stream."""
         self.join()
         N, M = self.num_envs, self.num_moves
-        if blocks and blocks > 0:
-            P = min(int(blocks), N)
-            i = torch.arange(N, device=self.device, dtype=torch.int64)
-            b = torch.zeros(N, device=self.device, dtype=torch.int64)
-            for g in range(1, P):
-                b += (i >= g * N // P).to(torch.int64)
-            self.timer.copy_(((b * M) // P % M).to(torch.int32))
+        if blocks == 1:
+            self.timer.zero_()
+        elif blocks and blocks > 0:
+            G = len(self._ranges)
+            Pg = max(1, -(-int(blocks) // G))
+            t = torch.zeros(N, dtype=torch.int64)
+            for g, (lo, hi) in enumerate(self._ranges):
+                n = hi - lo
+                for j in range(Pg):
+                    a, b = lo + j * n // Pg, lo + (j + 1) * n // Pg
+                    t[a:b] = (j * M // Pg + g * M // (Pg * G)) % M
+            self.timer.copy_(t.to(torch.int32).to(self.device))
         else:
             g = torch.arange(first_env, first_env + N, device=self.device, dtype=torch.int64)
             self.timer.copy_((g % M).to(torch.int32))
