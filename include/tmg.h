@@ -20,8 +20,10 @@
  *   n_new  int32 [n]   info["num_new_specials"]
  *   n_act  int32 [n]   info["num_specials_activated"]
  *   flags  uint8 [n]   bit0 done, bit1 is_combination_match, bit2 shuffled,
- *                      bit3 autoreset ran, bit6 internal capacity overflow,
- *                      bit7 error (step after done / bad action) tile_match_env.py:94-95
+ *                      bit3 autoreset ran, bit6 capacity overflow (more than
+ *                      4096 envs of one launch outgrew the LDS lists at once:
+ *                      that step is not exact), bit7 error (step after done /
+ *                      bad action, or an internal safety cap) tile_match_env.py:94-95
  *
  * Errors: 0 = ok, negative = error; tmg_last_error() gives a thread-local
  * message.  All launches are asynchronous on `stream` (a hipStream_t; NULL =
@@ -136,6 +138,12 @@ TMG_API int tmg_count_states(int device, int rows, int cols, int colours, uint64
 #define TMG_STATUS_OVERFLOW 2u
 #define TMG_STATUS_CALLER   4u
 TMG_API int tmg_status(tmg_ctx *ctx, uint32_t *status, int clear);
+
+/* Number of steps, since the context was created, whose cascade outgrew the
+ * general kernels' LDS lists and was re-run on global-memory lists sized for
+ * the worst case (spill_kernel; diagnostic — results are exact either way).
+ * Waits for the device. */
+TMG_API int tmg_spills(tmg_ctx *ctx, uint64_t *count);
 
 /* 1 when some rows x cols board with `colours` colours is line-free and has an
  * effective move, i.e. the reference's generate_board terminates

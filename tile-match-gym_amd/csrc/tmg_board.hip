@@ -80,6 +80,19 @@ enum : uint32_t { ST_INTERNAL = 1, ST_OVERFLOW = 2, ST_CALLER = 4 };
 #define TMG_MAX_SHUFFLES (1 << 12)   // shuffles per loop
 #endif
 
+// Per-stream queue of the envs whose step ran out of LDS list space (step_env)
+#ifndef TMG_SPILL_CAP
+#define TMG_SPILL_CAP 4096       // queued envs per step launch
+#endif
+#ifndef TMG_SPILL_WAVES
+#define TMG_SPILL_WAVES 8        // spill_kernel workgroups (one wave, one WsSerialBig each)
+#endif
+struct SpillQ {
+    uint32_t count, done;        // queued envs; spill_kernel waves finished
+    unsigned long long total;    // envs re-run so far (diagnostic, tmg_spills)
+    int64_t env[TMG_SPILL_CAP];
+};
+
 struct Params {
     int R, C, N, A, W, k, smask, num_moves;
     uint32_t thr;                 // Lemire threshold (2^32 - k) % k; 0 for powers of two
@@ -94,6 +107,8 @@ struct Params {
     uint64_t sb_in[2], sb_u[2], sb_v[2];   // cells of the board / of rows >= 1 / of rows >= 2
     const uint64_t *sb_rows;      // [R][4]: row r's cells (a, b), rows 0..r's cells (a, b)
     uint32_t *status;             // sticky status words, one per ST_* bit
+    SpillQ *spill;                // this launch's stream's spill queue (general kernels)
+    void *spill_ws;               // TMG_SPILL_WAVES WsSerialBig<MAXN> for spill_kernel
 };
 
 // host: the per-row masks of Params::sb_rows (boards of <= 128 cells)
@@ -123,6 +138,8 @@ inline Params make_params(int R, int C, int k, int smask, int num_moves, const u
     P.sb_z = 0;
     P.sb_rows = nullptr;
     P.status = nullptr;
+    P.spill = nullptr;
+    P.spill_ws = nullptr;
     if (P.N <= 128) {
         for (int p = 0; p < P.N; p++) {
             const int c = p % C, w = p & 1, b = p >> 1;
@@ -203,20 +220,18 @@ struct WsCore {
     } u;
 };
 
-// Capacities of the lane-0 lists.  A cascade step of a real board uses a few
-// dozen entries; the 512-cell workspace is sized at half the cell count so
-// the general 20x20 kernel fits twice the waves per CU in LDS.  Running out
-// sets FL_OVF (the step is then not trusted) rather than corrupting memory.
-template <int MAXN>
-struct WsSerial {                                   // lane-0 list machinery (general variant only)
-    static constexpr int CAP = MAXN > 128 ? MAXN / 2 : MAXN;
-    static constexpr int POOL = 4 * CAP + 256;      // coords of lines
-    static constexpr int MLINES = CAP + 64;         // lines
-    static constexpr int MQ = 2 * CAP + 64;         // process queue
-    static constexpr int MM = CAP + 32;             // matches
-    static constexpr int MPOOL = 4 * CAP + 256;     // coords of matches
-    static constexpr int MSTK = CAP + 8;            // activation DFS frames
-    static constexpr int MV = 96;                   // coords of one match
+// The lane-0 list machinery (general variant only): lines of get_colour_lines
+// (pool / ls / ll), the process queue (q), matches (ms / mlen / mname / mcol /
+// mpool), the activation DFS (f*), special placement (valid / taken / q*).
+template <int POOL_, int MLINES_, int MQ_, int MM_, int MPOOL_, int MSTK_>
+struct ListStore {
+    static constexpr int POOL = POOL_;              // coords of lines
+    static constexpr int MLINES = MLINES_;          // lines
+    static constexpr int MQ = MQ_;                  // process queue
+    static constexpr int MM = MM_;                  // matches
+    static constexpr int MPOOL = MPOOL_;            // coords of matches
+    static constexpr int MSTK = MSTK_;              // activation DFS frames
+    static constexpr int MV = 96;                   // coords of one match: a line (<= 64) + 3 bomb cells
     int16_t pool[POOL];
     int16_t ls[MLINES], ll[MLINES];
     int16_t q[MQ];
@@ -231,6 +246,32 @@ struct WsSerial {                                   // lane-0 list machinery (ge
     int32_t counts[16];
     int16_t pick[4];
 };
+
+// The LDS lists of the general kernels.  A cascade step of a real board uses a
+// few dozen entries; the 512-cell workspace is sized at half the cell count so
+// the general 20x20 kernel fits twice the waves per CU in LDS.  A step that
+// runs out (FL_OVF from the list machinery) is not written back: the env goes
+// to the spill queue and spill_kernel re-runs the step on WsSerialBig.
+template <int MAXN, int CAP = (MAXN > 128 ? MAXN / 2 : MAXN)>
+using WsSerial = ListStore<4 * CAP + 256, CAP + 64, 2 * CAP + 64, CAP + 32, 4 * CAP + 256, CAP + 8>;
+
+// Global-memory lists sized at the worst case of any board of <= MAXN cells
+// (R, C <= 64), so the spill re-run cannot run out.  One get_colour_lines
+// call (board.py:149-215) holds: first-pass lines of the bottom row, <= C
+// vertical + C/3 horizontal ones over <= N + C coords (a coord may be listed
+// twice); perpendicular lines, each holding exactly one coord (walks stop at
+// coords), so <= 2 per distinct coord (one per axis; a coord listed twice
+// repeats its lines, which the "not in lines" test drops), i.e. <= 2N; their
+// cells: every coord <= 2 times, every other cell <= 4 times (only the coords
+// closest to it along an axis, <= 2 per axis, reach it), i.e. <= 4N.  So the
+// pool holds <= 5N + C coords plus the R + C + 1 of the line being built.
+// process_colour_lines (:269-327) re-queues the tail of a cookie line (<= one
+// new line per 5 pooled coords), pops each queued line once and makes <= one
+// match per pop, whose coords are that line's plus <= 3 bomb cells.  The
+// activation DFS (:473-556) pushes a frame per special it enters, and entering
+// clears the cell, so <= N + 1 frames.
+template <int MAXN, int POOLB = 5 * MAXN + 3 * 64 + 64, int LINESB = 2 * MAXN + 2 * 64 + POOLB / 5 + 16>
+using WsSerialBig = ListStore<POOLB, LINESB, LINESB, LINESB, POOLB + 3 * LINESB, MAXN + 8>;
 
 template <int MAXN, bool GEN>
 struct Ws : WsCore<MAXN> {};
@@ -790,6 +831,16 @@ __device__ __forceinline__ int generate_board(const Params &P, WS &w, int lane, 
     return ensure_playable(P, w, lane, J, g, cl) & FL_ERR;
 }
 
+// Queue env e for spill_kernel; false when the queue is full.
+__device__ __forceinline__ bool spill_enqueue(const Params &P, int lane, int64_t e) {
+    int ok = 0;
+    if (lane == 0) {
+        const uint32_t i = atomicAdd(&P.spill->count, 1u);
+        if (i < (uint32_t)TMG_SPILL_CAP) { P.spill->env[i] = e; ok = 1; }
+    }
+    return __ballot(ok) != 0ULL;
+}
+
 // lane 0 records st in the sticky status words (a rare path: error / overflow)
 __device__ __forceinline__ void note_status(const Params &P, int lane, uint32_t st) {
 #if TMG_STATUS
@@ -886,18 +937,18 @@ __device__ __forceinline__ int fast_clear(const Params &P, WS &w, int lane, cons
 
 // ------------------------------------------------------------ general (lane 0)
 // Everything below runs on lane 0 only, against LDS.
-template <int MAXN>
+template <int MAXN, class LS = WsSerial<MAXN>>
 struct Serial {
     const Params &P;
     WsCore<MAXN> &w;
-    WsSerial<MAXN> &s;
+    LS &s;
     int8_t *col, *typ;
     int R, C, N;
     int nl, np;        // lines / pool fill
     int nm, nmp;       // matches / match-pool fill
     bool ovf;
 
-    __device__ __forceinline__ Serial(const Params &P_, WsCore<MAXN> &w_, WsSerial<MAXN> &s_) : P(P_), w(w_), s(s_) {
+    __device__ __forceinline__ Serial(const Params &P_, WsCore<MAXN> &w_, LS &s_) : P(P_), w(w_), s(s_) {
         R = P.R; C = P.C; N = P.N;
         col = w.brd; typ = w.brd + N;
         nl = np = nm = nmp = 0;
@@ -920,7 +971,7 @@ struct Serial {
                 int start = row - 1;
                 while (start > 0 && col[(start - 1) * C + c] == col[p]) start--;
                 if (row - start >= 2) {
-                    if (nl >= WsSerial<MAXN>::MLINES || np + (row - start + 1) > WsSerial<MAXN>::POOL) { ovf = true; return; }
+                    if (nl >= LS::MLINES || np + (row - start + 1) > LS::POOL) { ovf = true; return; }
                     s.ls[nl] = (int16_t)np; s.ll[nl] = (int16_t)(row - start + 1);
                     for (int i = start; i <= row; i++) s.pool[np++] = (int16_t)(i * C + c);
                     nl++;
@@ -930,7 +981,7 @@ struct Serial {
                 int end = c + 1;
                 while (end < C - 1 && col[row * C + end + 1] == col[p]) end++;
                 if (end - c >= 2) {
-                    if (nl >= WsSerial<MAXN>::MLINES || np + (end - c + 1) > WsSerial<MAXN>::POOL) { ovf = true; return; }
+                    if (nl >= LS::MLINES || np + (end - c + 1) > LS::POOL) { ovf = true; return; }
                     s.ls[nl] = (int16_t)np; s.ll[nl] = (int16_t)(end - c + 1);
                     for (int i = c; i <= end; i++) { s.pool[np++] = (int16_t)(row * C + i); hcov |= 1ULL << i; }
                     nl++;
@@ -947,7 +998,7 @@ struct Serial {
             const int cr = cp / C, cc = cp - cr * C;
             for (int d = 0; d < 2; d++) {
                 const int st = np;
-                if (np + R + C + 1 > WsSerial<MAXN>::POOL || nl >= WsSerial<MAXN>::MLINES) { ovf = true; break; }
+                if (np + R + C + 1 > LS::POOL || nl >= LS::MLINES) { ovf = true; break; }
                 s.pool[np++] = (int16_t)cp;
                 for (int sd = 0; sd < 2; sd++) {
                     int dr = d == 1 ? (sd ? -1 : 1) : 0, dc = d == 0 ? (sd ? -1 : 1) : 0;
@@ -990,12 +1041,12 @@ struct Serial {
     }
 
     __device__ __forceinline__ int add_match(int name, int colour) {
-        if (nm >= WsSerial<MAXN>::MM) { ovf = true; return -1; }
+        if (nm >= LS::MM) { ovf = true; return -1; }
         s.ms[nm] = (int16_t)nmp; s.mlen[nm] = 0; s.mname[nm] = (int8_t)name; s.mcol[nm] = (int8_t)colour;
         return nm++;
     }
     __device__ __forceinline__ void match_push(int m, int cell) {
-        if (nmp >= WsSerial<MAXN>::MPOOL) { ovf = true; return; }
+        if (nmp >= LS::MPOOL) { ovf = true; return; }
         s.mpool[nmp++] = (int16_t)cell; s.mlen[m]++;
     }
 
@@ -1019,7 +1070,7 @@ struct Serial {
                 int m = add_match(M_COOKIE, 0); if (m < 0) return;
                 for (int i = 0; i < 5; i++) match_push(m, s.pool[ls + i]);
                 if (ln - 5 > 2) {
-                    if (nl >= WsSerial<MAXN>::MLINES || qn >= WsSerial<MAXN>::MQ) { ovf = true; return; }
+                    if (nl >= LS::MLINES || qn >= LS::MQ) { ovf = true; return; }
                     s.ls[nl] = (int16_t)(ls + 5); s.ll[nl] = (int16_t)(ln - 5);
                     s.q[qn++] = (int16_t)nl; nl++;
                 }
@@ -1098,7 +1149,7 @@ struct Serial {
         if (t == 0 || t == 1) { w.sc[SC_ERR] = 1; return; }  // :491-492
         clr(cell);                                           // :496
         if (!combo) w.sc[SC_NACT]++;                         // :498-499
-        if (sp >= WsSerial<MAXN>::MSTK) { ovf = true; return; }
+        if (sp >= LS::MSTK) { ovf = true; return; }
         if (t == 2 || t == 3 || t == 4) {
             s.fcell[sp] = (int16_t)cell; s.ftype[sp] = (int8_t)t; s.fidx[sp] = 0; s.faux[sp] = 0; sp++;
         } else if (t == -1) {                                // :530-545
@@ -1166,7 +1217,7 @@ struct Serial {
         for (int i = 0; i < ml; i++) {
             int v = s.mpool[ms + i]; bool tk = false;
             for (int j = 0; j < nt; j++) if (taken[j] == v) { tk = true; break; }
-            if (!tk && nv < WsSerial<MAXN>::MV) valid[nv++] = (int16_t)v;
+            if (!tk && nv < LS::MV) valid[nv++] = (int16_t)v;
         }
         if (!straight) {
             int br = -1, bc = -1, bnr = -1, bnc = -1;
@@ -1201,7 +1252,7 @@ struct Serial {
         int16_t *qpos = s.qpos; int8_t *qname = s.qname, *qcol = s.qcol; int nq = 0;
         for (int m = 0; m < nm; m++) {
             if (s.mname[m] == M_NORMAL) continue;
-            if (nq >= WsSerial<MAXN>::MM) { ovf = true; return; }
+            if (nq >= LS::MM) { ovf = true; return; }
             int pos = creation_pos(m, taken, nt, s.mname[m] != M_BOMB);
             bool dup = false;
             for (int j = 0; j < nt; j++) if (taken[j] == pos) dup = true;
@@ -1297,9 +1348,10 @@ struct Serial {
 // Board.move, board.py:330-395 (the effectiveness test :352 is done by the
 // caller).  Returns eliminations; leaves the effective mask of the final
 // board in w.effw.
-template <int MAXN, bool GEN, int SBNB, bool CODD>
+template <int MAXN, bool GEN, int SBNB, bool CODD, class L>
 __device__ __forceinline__ int board_move(const Params &P, Ws<MAXN, GEN> &w, int lane, const LaneJump &J, Rng &g,
-                          const Cells<MAXN / 64> &cl, int p1, int p2, int &flags, int &nn, int &na, int64_t e) {
+                          const Cells<MAXN / 64> &cl, int p1, int p2, int &flags, int &nn, int &na, int64_t e,
+                          L *lists) {
     const int N = P.N;
     int8_t *col = w.brd, *typ = w.brd + N;
     int elim = 0;
@@ -1317,7 +1369,7 @@ __device__ __forceinline__ int board_move(const Params &P, Ws<MAXN, GEN> &w, int
             int nz = count_colour_nonzero(P, w, lane);
             if (lane == 0) {
                 w.sc[SC_NZ] = nz;
-                Serial<MAXN> S(P, w, w.s);
+                Serial<MAXN, L> S(P, w, *lists);
                 S.combination(p1, p2);
                 w.sc[SC_A] = S.ovf;
             }
@@ -1359,7 +1411,7 @@ __device__ __forceinline__ int board_move(const Params &P, Ws<MAXN, GEN> &w, int
                 int nz = count_colour_nonzero(P, w, lane);
                 if (lane == 0) {
                     w.sc[SC_NZ] = nz;
-                    Serial<MAXN> S(P, w, w.s);
+                    Serial<MAXN, L> S(P, w, *lists);
                     S.build_lines(rs);
                     if (!S.ovf) S.process_lines();
                     if (!S.ovf) S.resolve();
@@ -1416,12 +1468,12 @@ __device__ __forceinline__ void store_rng(uint64_t *p, const Rng &g, int lane) {
 // launch masked by FL_RESET (the 512-cell kernels: the reset kernel's
 // occupancy is far higher than the general step kernel's).  Returns the ST_*
 // bits this step raises for the sticky status word.
-template <int MAXN, bool GEN, int SBNB, bool CODD>
+template <int MAXN, bool GEN, int SBNB, bool CODD, bool SPILL = false, class L = WsSerial<MAXN>>
 __device__ __forceinline__ uint32_t step_env(
     const Params &P, Ws<MAXN, GEN> &w, int lane, int64_t e, int8_t *__restrict__ board, uint64_t *__restrict__ rng, int32_t *__restrict__ timer,
     const int32_t *__restrict__ actions, int32_t *__restrict__ reward, int32_t *__restrict__ n_new,
     int32_t *__restrict__ n_act, uint8_t *__restrict__ flags_out, uint64_t *__restrict__ eff, int trust_eff,
-    int autoreset) {
+    int autoreset, L *lists) {
     const int N = P.N, W = P.W;
     STAMP(e, 0);
     const int a = __builtin_amdgcn_readfirstlane(actions[e]);             // wave-uniform loads
@@ -1472,8 +1524,14 @@ __device__ __forceinline__ uint32_t step_env(
     STAMP(e, 1);
     if (effective) {
         if constexpr (SBNB > 0 && !GEN) elim = sb_move<SBNB, CODD>(P, w, lane, J, g, cl, p1, p2, flags, e);
-        else elim = board_move<MAXN, GEN, SBNB, CODD>(P, w, lane, J, g, cl, p1, p2, flags, nn, na, e);
+        else elim = board_move<MAXN, GEN, SBNB, CODD, L>(P, w, lane, J, g, cl, p1, p2, flags, nn, na, e, lists);
         changed = true;
+        if constexpr (GEN && !SPILL) {
+            // the LDS lists ran out: nothing of this env has been written; queue
+            // it for spill_kernel, which re-runs the whole step on lists sized
+            // for the worst case (a full queue leaves the step flagged FL_OVF)
+            if ((flags & FL_OVF) && spill_enqueue(P, lane, e)) return 0;
+        }
     }
     STAMP(e, 4);
     int tnew = t1;
@@ -1525,9 +1583,47 @@ __global__ TMG_LAUNCH_BOUNDS void step_kernel(
     WS &w = reinterpret_cast<WS *>(smem)[wv];
     const int64_t e = wg_env0() + wv;
     if (e >= n) return;
+    WsSerial<MAXN> *lists = nullptr;
+    if constexpr (GEN) lists = &w.s;
     const uint32_t st = step_env<MAXN, GEN, SBNB, CODD>(P, w, lane, e, board, rng, timer, actions, reward, n_new,
-                                                        n_act, flags_out, eff, trust_eff, autoreset);
+                                                        n_act, flags_out, eff, trust_eff, autoreset, lists);
     note_status(P, lane, st);
+}
+
+// Re-runs the steps the general step kernel queued on running out of LDS list
+// space (step_env, FL_OVF), on global-memory lists sized for the worst case
+// (WsSerialBig): launched right after every general step launch on the same
+// stream with the same buffers, TMG_SPILL_WAVES one-wave workgroups, each
+// with its own WsSerialBig.  An empty queue costs one load per wave.  The
+// generic (non-bitboard) path: bit-identical results by construction.
+template <int MAXN>
+__global__ __launch_bounds__(64) void spill_kernel(
+    Params P, int64_t n, int8_t *__restrict__ board, uint64_t *__restrict__ rng, int32_t *__restrict__ timer,
+    const int32_t *__restrict__ actions, int32_t *__restrict__ reward, int32_t *__restrict__ n_new,
+    int32_t *__restrict__ n_act, uint8_t *__restrict__ flags_out, uint64_t *__restrict__ eff, int trust_eff,
+    int autoreset) {
+    TMG_SMEM_DECL(smem);
+    using WS = Ws<MAXN, true>;
+    const int lane = threadIdx.x & 63;
+    WS &w = *reinterpret_cast<WS *>(smem);
+    SpillQ *q = P.spill;
+    WsSerialBig<MAXN> *lists = reinterpret_cast<WsSerialBig<MAXN> *>(P.spill_ws) + blockIdx.x;
+    const int cnt = min(__builtin_amdgcn_readfirstlane((int)q->count), TMG_SPILL_CAP);
+    int done = 0;
+    for (int i = (int)blockIdx.x; i < cnt; i += (int)gridDim.x) {
+        const int64_t e = (int64_t)bcast64((uint64_t)q->env[i]);
+        if (e < 0 || e >= n) continue;
+        WSYNC();
+        const uint32_t st = step_env<MAXN, true, 0, false, true, WsSerialBig<MAXN>>(
+            P, w, lane, e, board, rng, timer, actions, reward, n_new, n_act, flags_out, eff, trust_eff, autoreset, lists);
+        note_status(P, lane, st);
+        done++;
+    }
+    if (lane == 0) {
+        if (done) atomicAdd(&q->total, (unsigned long long)done);
+        __threadfence();
+        if (atomicAdd(&q->done, 1u) == gridDim.x - 1) { q->count = 0u; q->done = 0u; }   // the last wave empties the queue
+    }
 }
 
 // TileMatchEnv.reset without a seed (tile_match_env.py:84-91)

@@ -37,6 +37,14 @@ struct tmg_ctx {
     int maxn;
     int sb;          // scalar-bitboard kernels usable (<= 128 cells, C <= 63); TMG_SB=0 disables (A/B)
     int defer_general;   // 128-cell general kernel: autoreset by a masked reset launch (TMG_DEFER=0 disables)
+    // spill queues of the general kernels, one per stream the context steps on
+    // (a queue is only ever touched by the launches of its own stream, in order)
+    struct Spill {
+        hipStream_t stream;
+        tmg::SpillQ *q;
+        void *ws;
+    };
+    std::vector<Spill> spills;
 };
 
 using tmg::Params;
@@ -58,6 +66,33 @@ static void launch_step(dim3 grid, hipStream_t s, const Params &P, const StepArg
     const size_t lds = sizeof(tmg::Ws<MAXN, GEN>) * TMG_WPB;
     hipLaunchKernelGGL((tmg::step_kernel<MAXN, GEN, NB, CODD>), grid, dim3(64 * TMG_WPB), lds, s, P, a.n, a.board,
                        a.rng, a.timer, a.actions, a.reward, a.n_new, a.n_act, a.flags, a.eff, a.trust_eff, a.autoreset);
+}
+
+// the stream's spill queue (allocated zeroed on first use)
+static int spill_for(tmg_ctx *ctx, hipStream_t s, tmg::SpillQ **q, void **ws) {
+    for (const auto &x : ctx->spills)
+        if (x.stream == s) { *q = x.q; *ws = x.ws; return 0; }
+    const size_t wsz = ctx->maxn == 128 ? sizeof(tmg::WsSerialBig<128>) : sizeof(tmg::WsSerialBig<512>);
+    tmg_ctx::Spill sp{s, nullptr, nullptr};
+    int rc = hip_check(hipMalloc(&sp.q, sizeof(tmg::SpillQ)), "hipMalloc");
+    if (!rc) rc = hip_check(hipMalloc(&sp.ws, wsz * TMG_SPILL_WAVES), "hipMalloc");
+    if (!rc) rc = hip_check(hipMemset(sp.q, 0, sizeof(tmg::SpillQ)), "hipMemset");
+    if (rc) {
+        if (sp.q) (void)hipFree(sp.q);
+        if (sp.ws) (void)hipFree(sp.ws);
+        return rc;
+    }
+    ctx->spills.push_back(sp);
+    *q = sp.q;
+    *ws = sp.ws;
+    return 0;
+}
+
+template <int MAXN>
+static void launch_spill(hipStream_t s, const Params &P, const StepArgs &a) {
+    const size_t lds = sizeof(tmg::Ws<MAXN, true>);
+    hipLaunchKernelGGL((tmg::spill_kernel<MAXN>), dim3(TMG_SPILL_WAVES), dim3(64), lds, s, P, a.n, a.board, a.rng,
+                       a.timer, a.actions, a.reward, a.n_new, a.n_act, a.flags, a.eff, a.trust_eff, a.autoreset);
 }
 
 template <int MAXN, int NB, bool CODD>
@@ -121,11 +156,20 @@ static int do_reset(tmg_ctx *ctx, int64_t n, int8_t *board, uint64_t *rng, int32
 }
 
 static int do_step(tmg_ctx *ctx, StepArgs a, hipStream_t s) {
-    const Params &P = ctx->P;
-    const bool lean = P.smask == 0 && a.trust_eff;
+    const bool lean = ctx->P.smask == 0 && a.trust_eff;
+    Params P = ctx->P;
+    if (!lean) {                                   // general kernels: this stream's spill queue
+        int rc = spill_for(ctx, s, &P.spill, &P.spill_ws);
+        if (rc) return rc;
+    }
     const dim3 grid = env_grid(a.n);
     a.autoreset = a.autoreset ? 1 : 0;
-    if (ctx->maxn == 128 && !(ctx->defer_general && !lean && a.autoreset)) {
+    const int deferred = a.autoreset && (ctx->maxn == 512 || (ctx->defer_general && !lean));
+    // 512-cell kernels (and, with defer_general, the 128-cell general one):
+    // finished boards are regenerated by a reset_kernel launch masked by
+    // FL_RESET, which runs at several times the step kernel's occupancy
+    if (deferred) a.autoreset = 2;
+    if (ctx->maxn == 128) {
         if (ctx->sb) {
             if (lean) {
                 if (P.C & 1) launch_step_sb<false, true>(grid, s, P, a);
@@ -139,23 +183,20 @@ static int do_step(tmg_ctx *ctx, StepArgs a, hipStream_t s) {
         } else {
             launch_step<128, true, 0, false>(grid, s, P, a);
         }
-        return hip_check(hipGetLastError(), "kernel launch");
-    }
-    // 512-cell kernels (and, with defer_general, the 128-cell general one):
-    // finished boards are regenerated by a reset_kernel launch masked by
-    // FL_RESET, which runs at several times the step kernel's occupancy
-    const int deferred = a.autoreset;
-    if (deferred) a.autoreset = 2;
-    if (ctx->maxn == 128) {
-        if (P.C & 1) launch_step_sb<true, true>(grid, s, P, a);
-        else launch_step_sb<true, false>(grid, s, P, a);
     } else if (lean) {
         launch_step<512, false, 0, false>(grid, s, P, a);
     } else {
         launch_step<512, true, 0, false>(grid, s, P, a);
     }
     int rc = hip_check(hipGetLastError(), "kernel launch");
-    if (rc || !deferred) return rc;
+    if (rc) return rc;
+    if (!lean) {                                   // re-run the steps that ran out of LDS list space
+        if (ctx->maxn == 128) launch_spill<128>(s, P, a);
+        else launch_spill<512>(s, P, a);
+        rc = hip_check(hipGetLastError(), "kernel launch");
+        if (rc) return rc;
+    }
+    if (!deferred) return 0;
     return do_reset(ctx, a.n, a.board, a.rng, a.timer, a.eff, a.flags, tmg::FL_RESET, s);
 }
 
@@ -317,8 +358,28 @@ int tmg_destroy(tmg_ctx *ctx) {
     (void)hipFree(ctx->d_jump);
     (void)hipFree(ctx->d_status);
     if (ctx->d_sbrows) (void)hipFree(ctx->d_sbrows);
+    for (const auto &x : ctx->spills) {
+        (void)hipFree(x.q);
+        (void)hipFree(x.ws);
+    }
     delete ctx;
     return 0;
+}
+
+int tmg_spills(tmg_ctx *ctx, uint64_t *count) {
+    if (!count) return fail(-1, "null output pointer");
+    int rc = check_call(ctx, 0);
+    if (rc) return rc;
+    rc = hip_check(hipDeviceSynchronize(), "hipDeviceSynchronize");
+    uint64_t tot = 0;
+    for (const auto &x : ctx->spills) {
+        if (rc) break;
+        tmg::SpillQ h;
+        rc = hip_check(hipMemcpy(&h, x.q, 16, hipMemcpyDeviceToHost), "hipMemcpy");
+        tot += h.total;
+    }
+    if (!rc) *count = tot;
+    return rc;
 }
 
 int tmg_status(tmg_ctx *ctx, uint32_t *status, int clear) {

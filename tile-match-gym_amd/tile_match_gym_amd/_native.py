@@ -15,7 +15,7 @@ LIB_PATH = os.environ.get("TMG_LIB") or os.path.join(_HERE, "_lib", "libtmg.so")
 EXPORTS = ("tmg_create", "tmg_destroy", "tmg_reset", "tmg_step", "tmg_effective",
            "tmg_num_actions", "tmg_mask_words", "tmg_last_error", "tmg_abi_version",
            "tmg_onehot", "tmg_onehot_channels", "tmg_count_states", "tmg_sample_effective", "tmg_status",
-           "tmg_viable")
+           "tmg_viable", "tmg_spills")
 DTYPE_F32, DTYPE_U8, DTYPE_I32 = 0, 1, 2
 ABI_VERSION = 2
 STATUS_INTERNAL, STATUS_OVERFLOW, STATUS_CALLER = 1, 2, 4
@@ -59,9 +59,10 @@ def load():
     L.tmg_sample_effective.argtypes = [P, I64, P, ctypes.c_uint64, I64, ctypes.c_int32, P, P]
     L.tmg_status.argtypes = [P, ctypes.POINTER(ctypes.c_uint32), I]
     L.tmg_viable.argtypes = [I, I, I]
+    L.tmg_spills.argtypes = [P, ctypes.POINTER(ctypes.c_uint64)]
     for name in ("tmg_create", "tmg_destroy", "tmg_reset", "tmg_step", "tmg_effective",
                  "tmg_num_actions", "tmg_mask_words", "tmg_abi_version", "tmg_onehot", "tmg_onehot_channels",
-                 "tmg_sample_effective", "tmg_status", "tmg_viable",
+                 "tmg_sample_effective", "tmg_status", "tmg_viable", "tmg_spills",
                  "tmg_count_states"):
         getattr(L, name).restype = I
     if L.tmg_abi_version() != ABI_VERSION:
@@ -123,6 +124,12 @@ class Context:
         """Sticky STATUS_* bits of this context (waits for the device)."""
         v = ctypes.c_uint32(0)
         check(load().tmg_status(self._h, ctypes.byref(v), int(clear)))
+        return int(v.value)
+
+    def spills(self) -> int:
+        """Steps re-run on the worst-case global-memory lists so far (tmg_spills; waits for the device)."""
+        v = ctypes.c_uint64(0)
+        check(load().tmg_spills(self._h, ctypes.byref(v)))
         return int(v.value)
 
     def effective(self, n, board, eff, stream):

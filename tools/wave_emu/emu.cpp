@@ -202,8 +202,14 @@ static void run_blocks(int64_t n, size_t lds, F kernel) {
 }
 
 static uint64_t g_sbrows[64 * 4];
+static uint32_t g_status[4];
+static tmg::SpillQ g_spill;
+static std::vector<unsigned char> g_spill_ws(sizeof(tmg::WsSerialBig<512>) * TMG_SPILL_WAVES);
 static tmg::Params make_params(int R, int C, int k, int smask, int moves, const uint64_t *jump) {
     tmg::Params P = tmg::make_params(R, C, k, smask, moves, jump);
+    P.status = g_status;
+    P.spill = &g_spill;
+    P.spill_ws = g_spill_ws.data();
     if (P.N <= 128) {
         tmg::build_sb_rows(R, C, g_sbrows);
         P.sb_rows = g_sbrows;
@@ -232,6 +238,13 @@ template <int MAXN, bool GEN, int NB, bool CODD>
 static void emu_step_kernel(EmuStep &S) {
     const tmg::Params &P = *S.P;
     run_blocks(S.n, sizeof(tmg::Ws<MAXN, GEN>), [&] { tmg::step_kernel<MAXN, GEN, NB, CODD>(P, S.n, S.board, S.rng, S.timer, S.actions, S.reward, S.n_new, S.n_act, S.flags, S.eff, S.trust_eff, S.autoreset); });
+}
+
+// spill_kernel after a general step launch, as tmg_capi.hip's do_step
+template <int MAXN>
+static void emu_spill(EmuStep &S) {
+    const tmg::Params &P = *S.P;
+    run_grid(TMG_SPILL_WAVES, sizeof(tmg::Ws<MAXN, true>), [&] { tmg::spill_kernel<MAXN>(P, S.n, S.board, S.rng, S.timer, S.actions, S.reward, S.n_new, S.n_act, S.flags, S.eff, S.trust_eff, S.autoreset); });
 }
 
 template <bool GEN, bool CODD>
@@ -293,12 +306,14 @@ int emu_step(int R, int C, int k, int smask, int moves, int64_t n, int8_t *board
                 const int deferred = S.autoreset;
                 if (deferred) S.autoreset = 2;
                 if (P.C & 1) emu_step_sb<true, true>(S); else emu_step_sb<true, false>(S);
+                emu_spill<128>(S);
                 if (deferred) emu_do_reset(P, n, board, rng, timer, eff, flags, tmg::FL_RESET);
             }
         } else if (lean) {
             emu_step_kernel<128, false, 0, false>(S);
         } else {
             emu_step_kernel<128, true, 0, false>(S);
+            emu_spill<128>(S);
         }
         return 0;
     }
@@ -306,10 +321,16 @@ int emu_step(int R, int C, int k, int smask, int moves, int64_t n, int8_t *board
     const int deferred = S.autoreset;
     if (deferred) S.autoreset = 2;
     if (lean) emu_step_kernel<512, false, 0, false>(S);
-    else emu_step_kernel<512, true, 0, false>(S);
+    else {
+        emu_step_kernel<512, true, 0, false>(S);
+        emu_spill<512>(S);
+    }
     if (deferred) emu_do_reset(P, n, board, rng, timer, eff, flags, tmg::FL_RESET);
     return 0;
 }
+
+unsigned long long emu_spills(void) { return g_spill.total; }
+unsigned emu_status(void) { return (g_status[0] ? 1u : 0u) | (g_status[1] ? 2u : 0u) | (g_status[2] ? 4u : 0u); }
 
 int emu_reset(int R, int C, int k, int smask, int moves, int64_t n, int8_t *board, uint64_t *rng, int32_t *timer,
               uint64_t *eff) {

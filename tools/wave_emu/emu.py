@@ -21,6 +21,8 @@ def load(asan=False):
     L.emu_step.argtypes = [I, I, I, I, I, I64, P, P, P, P, P, P, P, P, P, I, I]
     L.emu_reset.argtypes = [I, I, I, I, I, I64, P, P, P, P]
     L.emu_effective.argtypes = [I, I, I, I, I64, P, P]
+    L.emu_spills.restype = ctypes.c_ulonglong
+    L.emu_status.restype = ctypes.c_uint
     return L
 
 

@@ -56,7 +56,9 @@ inline unsigned min(unsigned a, unsigned b) { return a < b ? a : b; }
 inline unsigned max(unsigned a, unsigned b) { return a > b ? a : b; }
 
 inline uint64_t __builtin_amdgcn_s_memrealtime() { return 0; }
-inline unsigned atomicOr(unsigned *p, unsigned v) { unsigned o = *p; *p |= v; return o; }
+inline unsigned atomicAdd(unsigned *p, unsigned v) { unsigned o = *p; *p += v; return o; }
+inline unsigned long long atomicAdd(unsigned long long *p, unsigned long long v) { unsigned long long o = *p; *p += v; return o; }
+inline void __threadfence() {}
 
 #define TMG_CONST_AS
 #define TMG_KEEP_V3(x, y, z) ((void)0)
