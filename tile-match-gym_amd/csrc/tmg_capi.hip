@@ -76,7 +76,9 @@ static int spill_for(tmg_ctx *ctx, hipStream_t s, tmg::SpillQ **q, void **ws) {
     tmg_ctx::Spill sp{s, nullptr, nullptr};
     int rc = hip_check(hipMalloc(&sp.q, sizeof(tmg::SpillQ)), "hipMalloc");
     if (!rc) rc = hip_check(hipMalloc(&sp.ws, wsz * TMG_SPILL_WAVES), "hipMalloc");
-    if (!rc) rc = hip_check(hipMemset(sp.q, 0, sizeof(tmg::SpillQ)), "hipMemset");
+    // zeroed in order on s itself (a memset on the null stream is not ordered
+    // with respect to a non-blocking stream's launches)
+    if (!rc) rc = hip_check(hipMemsetAsync(sp.q, 0, sizeof(tmg::SpillQ), s), "hipMemsetAsync");
     if (rc) {
         if (sp.q) (void)hipFree(sp.q);
         if (sp.ws) (void)hipFree(sp.ws);
@@ -328,6 +330,7 @@ int tmg_create(tmg_ctx **out, int device, int rows, int cols, int colours, uint3
     c->d_status = nullptr;
     rc = hip_check(hipMalloc(&c->d_status, 16), "hipMalloc");
     if (!rc) rc = hip_check(hipMemset(c->d_status, 0, 16), "hipMemset");
+    if (!rc) rc = hip_check(hipDeviceSynchronize(), "hipDeviceSynchronize");
     if (rc) {
         (void)hipFree(c->d_jump);
         if (c->d_status) (void)hipFree(c->d_status);
@@ -393,6 +396,7 @@ int tmg_status(tmg_ctx *ctx, uint32_t *status, int clear) {
     *status = (words[0] ? TMG_STATUS_INTERNAL : 0u) | (words[1] ? TMG_STATUS_OVERFLOW : 0u) |
               (words[2] ? TMG_STATUS_CALLER : 0u);
     if (clear) rc = hip_check(hipMemset(ctx->d_status, 0, sizeof words), "hipMemset");
+    if (clear && !rc) rc = hip_check(hipDeviceSynchronize(), "hipDeviceSynchronize");
     return rc;
 }
 
