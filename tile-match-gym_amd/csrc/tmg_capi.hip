@@ -45,6 +45,7 @@ struct tmg_ctx {
         void *ws;
     };
     std::vector<Spill> spills;
+    int spill_launch;    // TMG_SPILL=0 skips the spill launches (cost A/B only: overflowing steps are then lost)
 };
 
 using tmg::Params;
@@ -192,7 +193,7 @@ static int do_step(tmg_ctx *ctx, StepArgs a, hipStream_t s) {
     }
     int rc = hip_check(hipGetLastError(), "kernel launch");
     if (rc) return rc;
-    if (!lean) {                                   // re-run the steps that ran out of LDS list space
+    if (!lean && ctx->spill_launch) {              // re-run the steps that ran out of LDS list space
         if (ctx->maxn == 128) launch_spill<128>(s, P, a);
         else launch_spill<512>(s, P, a);
         rc = hip_check(hipGetLastError(), "kernel launch");
@@ -319,6 +320,8 @@ int tmg_create(tmg_ctx **out, int device, int rows, int cols, int colours, uint3
     const char *sbenv = getenv("TMG_SB");
     c->sb = P.N <= 128 && P.C <= 63 && !(sbenv && sbenv[0] == '0');
     c->defer_general = c->sb && !(denv && denv[0] == '0');
+    const char *spenv = getenv("TMG_SPILL");
+    c->spill_launch = !(spenv && spenv[0] == '0');
     uint64_t tab[64 * 4];
     tmg::build_jump_table(tab);
     rc = hip_check(hipMalloc(&c->d_jump, sizeof tab), "hipMalloc");
