@@ -109,6 +109,20 @@ TMG_API int tmg_effective(tmg_ctx *ctx, int64_t n, const int8_t *board, uint64_t
 TMG_API int tmg_onehot(tmg_ctx *ctx, int64_t n, const int8_t *board, void *out, int out_dtype, void *stream);
 TMG_API int tmg_onehot_channels(const tmg_ctx *ctx);
 
+/* tmg_step / tmg_reset with the one-hot planes fused into the kernels' own
+ * write-back (OneHotWrapper.observation, wrappers.py:50-69,
+ * applied to every step's obs): `onehot` is out[n][C_oh][R][C] as for
+ * tmg_onehot and must already hold the planes of the current boards (from a
+ * tmg_reset_onehot or a tmg_onehot call); a step rewrites the planes of every
+ * board it changes (any board when trust_eff == 0), tmg_reset_onehot those of
+ * every board it generates.  onehot == NULL: plain tmg_step / tmg_reset. */
+TMG_API int tmg_step_onehot(tmg_ctx *ctx, int64_t n, int8_t *board, uint64_t *rng, int32_t *timer,
+                            const int32_t *actions, int32_t *reward, int32_t *n_new, int32_t *n_act,
+                            uint8_t *flags, uint64_t *eff, int trust_eff, int autoreset, void *onehot,
+                            int onehot_dtype, void *stream);
+TMG_API int tmg_reset_onehot(tmg_ctx *ctx, int64_t n, int8_t *board, uint64_t *rng, int32_t *timer,
+                             uint64_t *eff, const uint8_t *env_mask, void *onehot, int onehot_dtype, void *stream);
+
 /* The examples' policy over info["effective_actions"] (src/examples/q_learning.py:19-25,
  * qrdqn.py:58), on device: actions[i] uniform over env i's effective actions
  * (the ascending list of tile_match_env.py:118-124, read from the bitmask eff

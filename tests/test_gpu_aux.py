@@ -140,3 +140,68 @@ def test_vector_env_autoreset_modes(mode):
         assert np.array_equal(obs["num_moves_left"].cpu().numpy(), moves - ref.timer), t
         mask = np.unpackbits(ref.eff.view(np.uint8).reshape(n, -1), axis=1, bitorder="little")[:, :A].astype(bool)
         assert np.array_equal(info["action_mask"].cpu().numpy(), mask), t
+
+
+def test_onehot_wrapper_reference_vectors():
+    """The reference's own OneHotWrapper expectations (tests/test_wrappers.py:5-41):
+    three seeded scenarios — colours after reset, a bomb made by action 33, a
+    cookie made by action 2 — replayed through this TileMatchEnv + OneHotWrapper,
+    asserting the reference's literal vectors and shapes."""
+    from tile_match_gym_amd.tile_match_env import TileMatchEnv
+    from tile_match_gym_amd.wrappers import OneHotWrapper
+    env = OneHotWrapper(TileMatchEnv(4, 3, 5, 10, [], [], seed=1))
+    assert env.observation_space["board"].shape == (5, 4, 3)
+    assert env.observation_space["num_moves_left"].n == 11
+    obs, info = env.reset()
+    assert np.array_equal(obs["board"][:, 0, 0], np.array([0, 0, 1, 0, 0], dtype=np.float32))
+    assert np.array_equal(obs["board"][:, 1, 1], np.array([1, 0, 0, 0, 0], dtype=np.float32))
+    assert obs["num_moves_left"] == 10
+
+    env = OneHotWrapper(TileMatchEnv(5, 5, 3, 10, [], ["bomb"], seed=2))
+    obs, info = env.reset()
+    assert np.array_equal(obs["board"][:, 2, 2], np.array([1, 0, 0, 0], dtype=np.float32))
+    obs, *_ = env.step(33)                                   # makes a bomb
+    assert obs["board"].shape == (4, 5, 5)
+    assert obs["num_moves_left"] == 9
+    assert np.array_equal(obs["board"][:, 3, 2], np.array([1, 0, 0, 1], dtype=np.float32))
+
+    env = OneHotWrapper(TileMatchEnv(5, 5, 2, 12, ["cookie"], ["vertical_laser"], seed=2))
+    obs, info = env.reset()
+    assert obs["board"].shape == (4, 5, 5)
+    assert obs["num_moves_left"] == 12
+    obs, *_ = env.step(2)                                    # makes a cookie
+    assert np.array_equal(obs["board"][:, 1, 2], np.array([0, 0, 1, 0], dtype=np.float32))
+    assert obs["board"].shape == (4, 5, 5)
+    assert obs["num_moves_left"] == 11
+
+
+@pytest.mark.parametrize("R,C,k,sm,groups", [(10, 10, 4, 0, 3), (10, 10, 4, 14, 2), (20, 20, 6, 15, 2),
+                                             (7, 5, 3, 1, 1), (6, 9, 5, 10, 1)])
+def test_fused_onehot_matches_separate_encode(R, C, k, sm, groups):
+    """tmg_step_onehot (one-hot planes written in the step / reset kernels'
+    own write-back, only for changed boards) == tmg_onehot of the boards after
+    every step, with autoreset, env groups, every dtype and a hand edit."""
+    from tile_match_gym_amd.shard import synthetic_actions
+    from tile_match_gym_amd.vec_env import TileMatchVecEnv
+    from tile_match_gym_amd.wrappers import VecOneHot
+    cl, co = _lists(sm)
+    n = 1500
+    for dt in (torch.float32, torch.uint8, torch.int32):
+        env = TileMatchVecEnv(n, R, C, k, 12, cl, co, seed=41, device=DEV, groups=groups)
+        env.reset()
+        fused = VecOneHot(env, dtype=dt, fused=True)
+        sep = VecOneHot(env, dtype=dt)
+        acts = torch.from_numpy(synthetic_actions(range(n), 30, env.num_actions)).to(DEV)
+        for t in range(30):
+            if t == 13:                                          # hand edit -> untrusted mask
+                env.join()
+                env.board[::7, 0, 0, 0] = 1
+                env.board[::7, 1, 0, 0] = 1
+                env.invalidate_effective_cache()
+            env.step_raw(acts[t])
+            got = fused.encode().clone()
+            want = sep.encode()
+            torch.cuda.synchronize()
+            assert torch.equal(got, want), (dt, t)
+        env.reset()                                              # tmg_reset_onehot
+        assert torch.equal(fused.encode().clone(), sep.encode()), dt

@@ -50,6 +50,9 @@ namespace tmg {
 #ifndef TMG_STATUS
 #define TMG_STATUS 1           // 0: no sticky status word (A/B of its cost only; tmg_status then reads 0)
 #endif
+#ifndef TMG_GEN128_WAVES
+#define TMG_GEN128_WAVES 4     // min waves per SIMD for the 128-cell general step kernel (caps it at 128 VGPRs)
+#endif
 #ifndef TMG_RESET512_WAVES
 #define TMG_RESET512_WAVES 4   // min waves per SIMD for the 512-cell reset kernel (caps its VGPRs)
 #endif
@@ -107,6 +110,9 @@ struct Params {
     uint64_t sb_in[2], sb_u[2], sb_v[2];   // cells of the board / of rows >= 1 / of rows >= 2
     const uint64_t *sb_rows;      // [R][4]: row r's cells (a, b), rows 0..r's cells (a, b)
     uint32_t *status;             // sticky status words, one per ST_* bit
+    void *oh;                     // fused OneHotWrapper output [n][oh_ch][R][C], or null (tmg_step_onehot)
+    int oh_dtype, oh_ch, oh_nsel; // TMG_DTYPE_*; channels = k + nsel
+    uint32_t oh_sel;              // type ids of the special channels, int8 each (wrappers.py:37-46)
     SpillQ *spill;                // this launch's stream's spill queue (general kernels)
     void *spill_ws;               // TMG_SPILL_WAVES WsSerialBig<MAXN> for spill_kernel
 };
@@ -140,6 +146,9 @@ inline Params make_params(int R, int C, int k, int smask, int num_moves, const u
     P.status = nullptr;
     P.spill = nullptr;
     P.spill_ws = nullptr;
+    P.oh = nullptr;
+    P.oh_dtype = P.oh_ch = P.oh_nsel = 0;
+    P.oh_sel = 0;
     if (P.N <= 128) {
         for (int p = 0; p < P.N; p++) {
             const int c = p % C, w = p & 1, b = p >> 1;
@@ -460,6 +469,27 @@ __device__ __forceinline__ void store_board(const Params &P, const WS &w, int la
         for (int i = lane; i < (nb >> 2); i += 64) d[i] = s[i];
     } else {
         for (int i = lane; i < nb; i += 64) dst[i] = w.brd[i];
+    }
+}
+
+// OneHotWrapper._one_hot_encode_board (wrappers.py:56-69) of env e's board in
+// LDS, written in the step's own write-back: channel c < k is (colour == c+1),
+// channel k + j is (type == oh_sel[j]); each channel's stores are coalesced.
+// A one is 1.0f (0x3f800000) for f32, 1 for u8 / i32.
+template <class WS>
+__device__ __forceinline__ void store_onehot(const Params &P, const WS &w, int lane, int64_t e) {
+    const int N = P.N, k = P.k, ch = P.oh_ch;
+    const bool bytes = P.oh_dtype == 1;
+    const uint32_t one = P.oh_dtype == 0 ? 0x3f800000u : 1u;
+    uint8_t *o8 = reinterpret_cast<uint8_t *>(P.oh) + e * (int64_t)ch * N;
+    uint32_t *o32 = reinterpret_cast<uint32_t *>(P.oh) + e * (int64_t)ch * N;
+    for (int p = lane; p < N; p += 64) {
+        const int x = w.brd[p], y = w.brd[N + p];
+        for (int c = 0; c < ch; c++) {
+            const bool on = c < k ? x == c + 1 : y == (int)(int8_t)(P.oh_sel >> (8 * (c - k)));
+            if (bytes) o8[c * N + p] = on ? 1 : 0;
+            else o32[c * N + p] = on ? one : 0u;
+        }
     }
 }
 
@@ -1549,6 +1579,9 @@ __device__ __forceinline__ uint32_t step_env(
         store_board(P, w, lane, gb);
         store_rng(rng + e * 5, g, lane);
     }
+    // fused one-hot planes: every board this step changed (or, with an
+    // untrusted mask, any board: it may have been edited by hand)
+    if (P.oh && (changed || !trust_eff)) store_onehot(P, w, lane, e);
     if (done && !autoreset) {
         for (int i = lane; i < W; i += 64) ge[i] = 0ULL;                   // tile_match_env.py:119-120
     } else if (changed) {
@@ -1571,7 +1604,7 @@ __device__ __forceinline__ uint32_t step_env(
 
 // TileMatchEnv.step over a batch, one wave per env.
 template <int MAXN, bool GEN, int SBNB = 0, bool CODD = false>
-__global__ TMG_LAUNCH_BOUNDS void step_kernel(
+__global__ __launch_bounds__(64 * TMG_WPB, (MAXN == 128 && GEN) ? TMG_GEN128_WAVES : TMG_WPE) void step_kernel(
     Params P, int64_t n, int8_t *__restrict__ board, uint64_t *__restrict__ rng, int32_t *__restrict__ timer,
     const int32_t *__restrict__ actions, int32_t *__restrict__ reward, int32_t *__restrict__ n_new,
     int32_t *__restrict__ n_act, uint8_t *__restrict__ flags_out, uint64_t *__restrict__ eff, int trust_eff,
@@ -1650,6 +1683,7 @@ __global__ __launch_bounds__(64 * TMG_WPB, MAXN > 128 ? TMG_RESET512_WAVES : 1) 
     note_status(P, lane, fl ? ST_INTERNAL : 0u);
     store_board(P, w, lane, board + e * 2 * N);
     store_rng(rng + e * 5, g, lane);
+    if (P.oh) store_onehot(P, w, lane, e);
     for (int i = lane; i < W; i += 64) eff[e * W + i] = w.effw[i];
     if (lane == 0) timer[e] = 0;
 }

@@ -141,9 +141,8 @@ static int set_device(tmg_ctx *ctx) {
     return 0;
 }
 
-static int do_reset(tmg_ctx *ctx, int64_t n, int8_t *board, uint64_t *rng, int32_t *timer, uint64_t *eff,
-                    const uint8_t *env_mask, int mask_bits, hipStream_t s) {
-    const Params &P = ctx->P;
+static int do_reset(tmg_ctx *ctx, const Params &P, int64_t n, int8_t *board, uint64_t *rng, int32_t *timer,
+                    uint64_t *eff, const uint8_t *env_mask, int mask_bits, hipStream_t s) {
     const dim3 grid = env_grid(n);
     if (ctx->maxn == 128) {
         if (ctx->sb) {
@@ -158,9 +157,8 @@ static int do_reset(tmg_ctx *ctx, int64_t n, int8_t *board, uint64_t *rng, int32
     return hip_check(hipGetLastError(), "kernel launch");
 }
 
-static int do_step(tmg_ctx *ctx, StepArgs a, hipStream_t s) {
+static int do_step(tmg_ctx *ctx, Params P, StepArgs a, hipStream_t s) {
     const bool lean = ctx->P.smask == 0 && a.trust_eff;
-    Params P = ctx->P;
     if (!lean) {                                   // general kernels: this stream's spill queue
         int rc = spill_for(ctx, s, &P.spill, &P.spill_ws);
         if (rc) return rc;
@@ -200,7 +198,7 @@ static int do_step(tmg_ctx *ctx, StepArgs a, hipStream_t s) {
         if (rc) return rc;
     }
     if (!deferred) return 0;
-    return do_reset(ctx, a.n, a.board, a.rng, a.timer, a.eff, a.flags, tmg::FL_RESET, s);
+    return do_reset(ctx, P, a.n, a.board, a.rng, a.timer, a.eff, a.flags, tmg::FL_RESET, s);
 }
 
 static int do_effective(tmg_ctx *ctx, int64_t n, const int8_t *board, uint64_t *eff, hipStream_t s) {
@@ -408,32 +406,6 @@ int tmg_viable(int rows, int cols, int colours) {
     return shape_viable(rows, cols, colours) ? 1 : 0;
 }
 
-int tmg_reset(tmg_ctx *ctx, int64_t n, int8_t *board, uint64_t *rng, int32_t *timer, uint64_t *eff,
-              const uint8_t *env_mask, void *stream) {
-    if (!board || !rng || !timer || !eff) return fail(-1, "null state buffer");
-    int rc = check_call(ctx, n);
-    if (rc || n == 0) return rc;
-    return do_reset(ctx, n, board, rng, timer, eff, env_mask, 0xFF, reinterpret_cast<hipStream_t>(stream));
-}
-
-int tmg_step(tmg_ctx *ctx, int64_t n, int8_t *board, uint64_t *rng, int32_t *timer, const int32_t *actions,
-             int32_t *reward, int32_t *n_new, int32_t *n_act, uint8_t *flags, uint64_t *eff, int trust_eff,
-             int autoreset, void *stream) {
-    if (!board || !rng || !timer || !actions || !reward || !n_new || !n_act || !flags || !eff)
-        return fail(-1, "null buffer");
-    int rc = check_call(ctx, n);
-    if (rc || n == 0) return rc;
-    const StepArgs a{n, board, rng, timer, actions, reward, n_new, n_act, flags, eff, trust_eff, autoreset};
-    return do_step(ctx, a, reinterpret_cast<hipStream_t>(stream));
-}
-
-int tmg_effective(tmg_ctx *ctx, int64_t n, const int8_t *board, uint64_t *eff, void *stream) {
-    if (!board || !eff) return fail(-1, "null buffer");
-    int rc = check_call(ctx, n);
-    if (rc || n == 0) return rc;
-    return do_effective(ctx, n, board, eff, reinterpret_cast<hipStream_t>(stream));
-}
-
 // OneHotWrapper channel selection (wrappers.py:39-46): enabled specials as
 // type ids, in the order of sorted(id + 1)
 static int onehot_sel(uint32_t smask, int ids[4]) {
@@ -443,6 +415,66 @@ static int onehot_sel(uint32_t smask, int ids[4]) {
     if (smask & TMG_SPECIAL_HLASER) ids[n++] = 3;
     if (smask & TMG_SPECIAL_BOMB) ids[n++] = 4;
     return n;
+}
+
+// Params of a call with the fused one-hot output `onehot` (null: none)
+static int onehot_params(tmg_ctx *ctx, void *onehot, int dtype, Params &P) {
+    P = ctx->P;
+    if (!onehot) return 0;
+    if (dtype != TMG_DTYPE_F32 && dtype != TMG_DTYPE_U8 && dtype != TMG_DTYPE_I32)
+        return fail(-2, "unknown one-hot output dtype");
+    int ids[4] = {0, 0, 0, 0};
+    P.oh_nsel = onehot_sel((uint32_t)P.smask, ids);
+    P.oh_sel = 0;
+    for (int i = 0; i < 4; i++) P.oh_sel |= (uint32_t)(uint8_t)(int8_t)ids[i] << (8 * i);
+    P.oh_ch = P.k + P.oh_nsel;
+    P.oh_dtype = dtype;
+    P.oh = onehot;
+    return 0;
+}
+
+int tmg_reset(tmg_ctx *ctx, int64_t n, int8_t *board, uint64_t *rng, int32_t *timer, uint64_t *eff,
+              const uint8_t *env_mask, void *stream) {
+    return tmg_reset_onehot(ctx, n, board, rng, timer, eff, env_mask, nullptr, 0, stream);
+}
+
+int tmg_reset_onehot(tmg_ctx *ctx, int64_t n, int8_t *board, uint64_t *rng, int32_t *timer, uint64_t *eff,
+                     const uint8_t *env_mask, void *onehot, int onehot_dtype, void *stream) {
+    if (!board || !rng || !timer || !eff) return fail(-1, "null state buffer");
+    int rc = check_call(ctx, n);
+    if (rc || n == 0) return rc;
+    Params P;
+    rc = onehot_params(ctx, onehot, onehot_dtype, P);
+    if (rc) return rc;
+    return do_reset(ctx, P, n, board, rng, timer, eff, env_mask, 0xFF, reinterpret_cast<hipStream_t>(stream));
+}
+
+int tmg_step(tmg_ctx *ctx, int64_t n, int8_t *board, uint64_t *rng, int32_t *timer, const int32_t *actions,
+             int32_t *reward, int32_t *n_new, int32_t *n_act, uint8_t *flags, uint64_t *eff, int trust_eff,
+             int autoreset, void *stream) {
+    return tmg_step_onehot(ctx, n, board, rng, timer, actions, reward, n_new, n_act, flags, eff, trust_eff, autoreset,
+                           nullptr, 0, stream);
+}
+
+int tmg_step_onehot(tmg_ctx *ctx, int64_t n, int8_t *board, uint64_t *rng, int32_t *timer, const int32_t *actions,
+                    int32_t *reward, int32_t *n_new, int32_t *n_act, uint8_t *flags, uint64_t *eff, int trust_eff,
+                    int autoreset, void *onehot, int onehot_dtype, void *stream) {
+    if (!board || !rng || !timer || !actions || !reward || !n_new || !n_act || !flags || !eff)
+        return fail(-1, "null buffer");
+    int rc = check_call(ctx, n);
+    if (rc || n == 0) return rc;
+    Params P;
+    rc = onehot_params(ctx, onehot, onehot_dtype, P);
+    if (rc) return rc;
+    const StepArgs a{n, board, rng, timer, actions, reward, n_new, n_act, flags, eff, trust_eff, autoreset};
+    return do_step(ctx, P, a, reinterpret_cast<hipStream_t>(stream));
+}
+
+int tmg_effective(tmg_ctx *ctx, int64_t n, const int8_t *board, uint64_t *eff, void *stream) {
+    if (!board || !eff) return fail(-1, "null buffer");
+    int rc = check_call(ctx, n);
+    if (rc || n == 0) return rc;
+    return do_effective(ctx, n, board, eff, reinterpret_cast<hipStream_t>(stream));
 }
 
 int tmg_onehot_channels(const tmg_ctx *ctx) {

@@ -15,7 +15,7 @@ LIB_PATH = os.environ.get("TMG_LIB") or os.path.join(_HERE, "_lib", "libtmg.so")
 EXPORTS = ("tmg_create", "tmg_destroy", "tmg_reset", "tmg_step", "tmg_effective",
            "tmg_num_actions", "tmg_mask_words", "tmg_last_error", "tmg_abi_version",
            "tmg_onehot", "tmg_onehot_channels", "tmg_count_states", "tmg_sample_effective", "tmg_status",
-           "tmg_viable", "tmg_spills")
+           "tmg_viable", "tmg_spills", "tmg_step_onehot", "tmg_reset_onehot")
 DTYPE_F32, DTYPE_U8, DTYPE_I32 = 0, 1, 2
 ABI_VERSION = 2
 STATUS_INTERNAL, STATUS_OVERFLOW, STATUS_CALLER = 1, 2, 4
@@ -60,9 +60,11 @@ def load():
     L.tmg_status.argtypes = [P, ctypes.POINTER(ctypes.c_uint32), I]
     L.tmg_viable.argtypes = [I, I, I]
     L.tmg_spills.argtypes = [P, ctypes.POINTER(ctypes.c_uint64)]
+    L.tmg_step_onehot.argtypes = [P, I64, P, P, P, P, P, P, P, P, P, I, I, P, I, P]
+    L.tmg_reset_onehot.argtypes = [P, I64, P, P, P, P, P, P, I, P]
     for name in ("tmg_create", "tmg_destroy", "tmg_reset", "tmg_step", "tmg_effective",
                  "tmg_num_actions", "tmg_mask_words", "tmg_abi_version", "tmg_onehot", "tmg_onehot_channels",
-                 "tmg_sample_effective", "tmg_status", "tmg_viable", "tmg_spills",
+                 "tmg_sample_effective", "tmg_status", "tmg_viable", "tmg_spills", "tmg_step_onehot", "tmg_reset_onehot",
                  "tmg_count_states"):
         getattr(L, name).restype = I
     if L.tmg_abi_version() != ABI_VERSION:
@@ -113,12 +115,23 @@ class Context:
         except Exception:
             pass
 
-    def reset(self, n, board, rng, timer, eff, env_mask, stream):
-        check(load().tmg_reset(self._h, int(n), board, rng, timer, eff, env_mask, stream))
+    def reset(self, n, board, rng, timer, eff, env_mask, stream, onehot=None, onehot_dtype=DTYPE_F32):
+        """tmg_reset, or tmg_reset_onehot when a fused one-hot output pointer is given."""
+        if onehot:
+            check(load().tmg_reset_onehot(self._h, int(n), board, rng, timer, eff, env_mask, onehot,
+                                          int(onehot_dtype), stream))
+        else:
+            check(load().tmg_reset(self._h, int(n), board, rng, timer, eff, env_mask, stream))
 
-    def step(self, n, board, rng, timer, actions, reward, n_new, n_act, flags, eff, trust_eff, autoreset, stream):
-        check(load().tmg_step(self._h, int(n), board, rng, timer, actions, reward, n_new, n_act, flags, eff,
-                              int(trust_eff), int(autoreset), stream))
+    def step(self, n, board, rng, timer, actions, reward, n_new, n_act, flags, eff, trust_eff, autoreset, stream,
+             onehot=None, onehot_dtype=DTYPE_F32):
+        """tmg_step, or tmg_step_onehot when a fused one-hot output pointer is given."""
+        if onehot:
+            check(load().tmg_step_onehot(self._h, int(n), board, rng, timer, actions, reward, n_new, n_act, flags,
+                                         eff, int(trust_eff), int(autoreset), onehot, int(onehot_dtype), stream))
+        else:
+            check(load().tmg_step(self._h, int(n), board, rng, timer, actions, reward, n_new, n_act, flags, eff,
+                                  int(trust_eff), int(autoreset), stream))
 
     def status(self, clear: bool = False) -> int:
         """Sticky STATUS_* bits of this context (waits for the device)."""

@@ -88,6 +88,8 @@ class TileMatchVecEnv:
         self.n_act = torch.zeros(N, dtype=torch.int32, **kw)
         self.flags = torch.zeros(N, dtype=torch.uint8, **kw)
         self.actions = None                     # step_effective's sampled actions (N,) int32
+        self.onehot = None                      # fused one-hot planes (attach_onehot)
+        self._oh_code = _native.DTYPE_F32
         self._eff_valid = False
         groups = max(1, min(int(groups), N))
         self.groups = groups
@@ -177,7 +179,7 @@ class TileMatchVecEnv:
         if env_mask is not None:
             m = torch.as_tensor(env_mask, device=self.device).to(torch.uint8).contiguous()
         self.ctx.reset(self.num_envs, _ptr(self.board), _ptr(self.rng), _ptr(self.timer), _ptr(self.eff),
-                       _ptr(m), self._stream())
+                       _ptr(m), self._stream(), self._oh(0), self._oh_code)
         self._eff_valid = True
         return self._obs(), {"effective_bits": self.eff}
 
@@ -211,14 +213,14 @@ class TileMatchVecEnv:
         if not self._streams:
             self.ctx.step(self.num_envs, _ptr(self.board), _ptr(self.rng), _ptr(self.timer), _ptr(actions_i32),
                           _ptr(self.reward), _ptr(self.n_new), _ptr(self.n_act), _ptr(self.flags), _ptr(self.eff),
-                          trust, auto, self._stream())
+                          trust, auto, self._stream(), self._oh(0), self._oh_code)
         else:
             self._fork()
             a0 = actions_i32.data_ptr()
             for (lo, _), st, p in zip(self._ranges, self._streams, self._gptr):
                 actions_i32.record_stream(st)
                 self.ctx.step(p[0], p[1], p[2], p[3], a0 + 4 * lo, p[5], p[6], p[7], p[8], p[4], trust, auto,
-                              st.cuda_stream)
+                              st.cuda_stream, self._oh(lo), self._oh_code)
         self._eff_valid = True
 
     def step_effective(self, t: int, key: int = 12345, first_env: int = 0):
@@ -238,13 +240,13 @@ class TileMatchVecEnv:
             self.ctx.sample_effective(self.num_envs, _ptr(self.eff), key, first_env, t, act, s)
             self.ctx.step(self.num_envs, _ptr(self.board), _ptr(self.rng), _ptr(self.timer), act,
                           _ptr(self.reward), _ptr(self.n_new), _ptr(self.n_act), _ptr(self.flags), _ptr(self.eff),
-                          trust, auto, s)
+                          trust, auto, s, self._oh(0), self._oh_code)
         else:
             self._fork()
             for (lo, _), st, p in zip(self._ranges, self._streams, self._gptr):
                 self.ctx.sample_effective(p[0], p[4], key, first_env + lo, t, act + 4 * lo, st.cuda_stream)
                 self.ctx.step(p[0], p[1], p[2], p[3], act + 4 * lo, p[5], p[6], p[7], p[8], p[4], trust, auto,
-                              st.cuda_stream)
+                              st.cuda_stream, self._oh(lo), self._oh_code)
         self._eff_valid = True
 
     def invalidate_effective_cache(self):
@@ -262,6 +264,33 @@ class TileMatchVecEnv:
         bits = torch.arange(64, device=self.device, dtype=torch.int64)
         m = ((self.eff.unsqueeze(-1) >> bits) & 1).reshape(self.num_envs, -1)[:, :self.num_actions]
         return m.bool()
+
+    # ------------------------------------------------------ fused one-hot
+    def attach_onehot(self, dtype=torch.float32) -> torch.Tensor:
+        """Keep OneHotWrapper planes (wrappers.py:56-69) of every board in a
+        (N, channels, R, C) tensor that the step / reset kernels update in
+        their own write-back (tmg_step_onehot): only boards a step changes are
+        rewritten.  Encodes the current boards once (tmg_onehot); returns the
+        tensor (also self.onehot).  Call refresh_onehot() after editing boards
+        by hand with a trusted mask."""
+        codes = {torch.float32: _native.DTYPE_F32, torch.uint8: _native.DTYPE_U8, torch.int32: _native.DTYPE_I32}
+        if dtype not in codes:
+            raise ValueError(f"dtype must be one of {list(codes)}")
+        self.join()
+        ch = self.ctx.onehot_channels()
+        self.onehot = torch.zeros((self.num_envs, ch, self.num_rows, self.num_cols), dtype=dtype, device=self.device)
+        self._oh_code = codes[dtype]
+        self.refresh_onehot()
+        return self.onehot
+
+    def refresh_onehot(self):
+        self.join()
+        self.ctx.onehot(self.num_envs, self.board.data_ptr(), self.onehot.data_ptr(), self._oh_code, self._stream())
+
+    def _oh(self, lo):
+        if self.onehot is None:
+            return None
+        return self.onehot.data_ptr() + lo * self.onehot[0].numel() * self.onehot.element_size()
 
     def _obs(self):
         return {"board": self.board, "num_moves_left": self.num_moves - self.timer}

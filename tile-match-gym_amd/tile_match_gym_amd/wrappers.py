@@ -123,19 +123,30 @@ class ProportionRewardWrapper(_Wrapper):
 
 
 class VecOneHot:
-    """One-hot boards of a TileMatchVecEnv: `encode()` -> (N, channels, R, C) on the env's device."""
+    """One-hot boards of a TileMatchVecEnv: `encode()` -> (N, channels, R, C) on the env's device.
 
-    def __init__(self, vec_env, dtype=torch.float32):
+    fused=True: the planes are kept by the step / reset kernels themselves
+    (TileMatchVecEnv.attach_onehot -> tmg_step_onehot), rewritten only for
+    the boards a step changes; `encode()` then just returns them."""
+
+    def __init__(self, vec_env, dtype=torch.float32, fused=False):
         if dtype not in _TORCH_DTYPES:
             raise ValueError(f"dtype must be one of {list(_TORCH_DTYPES)}")
         self.env = vec_env
         self.dtype = dtype
+        self.fused = bool(fused)
         self.channels = vec_env.ctx.onehot_channels()
         self.type_slices = _type_slices(vec_env.colourless_specials, vec_env.colour_specials)
-        self.out = torch.empty((vec_env.num_envs, self.channels, vec_env.num_rows, vec_env.num_cols), dtype=dtype,
-                               device=vec_env.device)
+        if self.fused:
+            self.out = vec_env.attach_onehot(dtype)
+        else:
+            self.out = torch.empty((vec_env.num_envs, self.channels, vec_env.num_rows, vec_env.num_cols),
+                                   dtype=dtype, device=vec_env.device)
 
     def encode(self, board=None) -> torch.Tensor:
+        if self.fused and board is None:
+            self.env.join()
+            return self.out
         b = self.env.board if board is None else board
         if b.dtype != torch.int8 or not b.is_contiguous() or b.shape != self.env.board.shape:
             raise ValueError("board must be a contiguous int8 (N, 2, R, C) tensor")
