@@ -9,9 +9,11 @@ GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
 SHAPE_KEYS = ("R", "C", "k", "smask")
 
 
-def load_records(name):
-    """fn_<name>.npz -> list of dict records (see make_goldens.pack_records)."""
-    z = np.load(os.path.join(GOLDEN, f"fn_{name}.npz"), allow_pickle=False)
+def load_records(name, prefix="fn"):
+    """<prefix>_<name>.npz -> list of dict records (see make_goldens.pack_records).
+    prefix "fn": random boards (make_goldens.py); "ref": the reference's own
+    hand-built test boards (make_ref_cases.py)."""
+    z = np.load(os.path.join(GOLDEN, f"{prefix}_{name}.npz"), allow_pickle=False)
     n = int(z["n"])
     keys = [k for k in z.files if k not in ("n",) and not k.endswith("_off")]
     recs = []

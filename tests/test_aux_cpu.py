@@ -66,3 +66,33 @@ def test_policy_restatement_properties():
     one[:] = np.uint64(0b1011)                                  # actions {0, 1, 3}
     c = np.bincount(sample_effective_np(one, 64, 9, 0, 0), minlength=4)
     assert c[2] == 0 and all(abs(c[i] - 20000 / 3) < 400 for i in (0, 1, 3))
+
+
+def test_checkpoint_format_roundtrip_oracle(tmp_path):
+    """The checkpoint file (vec_env.save_state / load_state: .npz of the
+    include/tmg.h arrays + JSON config, no pickle) carries the exact PCG64
+    stream position incl. numpy's buffered half-word: an oracle batch restored
+    from it continues exactly like the uninterrupted one."""
+    import numpy as np
+    from oracle import oracle as orc
+    from tile_match_gym_amd.seeding import batch_rng_words
+    from tile_match_gym_amd.shard import synthetic_actions
+    from tile_match_gym_amd.vec_env import load_state, save_state
+    n, R, C, k, sm = 256, 8, 8, 3, 15
+    a = orc.OracleBatch(R, C, k, sm, 12, batch_rng_words(range(50, 50 + n)))
+    a.reset()
+    acts = synthetic_actions(range(n), 40, a.A)
+    for t in range(17):
+        a.step(acts[t])
+    p = tmp_path / "ck.npz"
+    save_state(p, {"board": a.board, "rng": a.rng, "timer": a.timer, "eff": a.eff}, {"num_rows": R})
+    arrays, cfg = load_state(p)
+    assert cfg["num_rows"] == R and cfg["format"] == 1
+    assert ((arrays["rng"][:, 4] >> np.uint64(32)) & np.uint64(1)).any()
+    b = orc.OracleBatch(R, C, k, sm, 12, arrays["rng"])
+    b.board[:], b.timer[:], b.eff[:] = arrays["board"], arrays["timer"], arrays["eff"]
+    for t in range(17, 40):
+        a.step(acts[t])
+        b.step(acts[t])
+        for f in ("board", "rng", "timer", "eff", "reward", "flags"):
+            assert np.array_equal(getattr(a, f), getattr(b, f)), (t, f)

@@ -205,3 +205,38 @@ def test_fused_onehot_matches_separate_encode(R, C, k, sm, groups):
             assert torch.equal(got, want), (dt, t)
         env.reset()                                              # tmg_reset_onehot
         assert torch.equal(fused.encode().clone(), sep.encode()), dt
+
+
+def test_checkpoint_restore_vs_oracle(tmp_path):
+    """Save mid-episode on the GPU, load the arrays into the oracle (board, the
+    PCG64 words incl. numpy's buffered half-word and its flag, timer, eff) and
+    into a fresh TileMatchVecEnv; 35 more steps (two autoresets) must agree
+    with the oracle at every step (tile_match_env.py:49 stream format)."""
+    from tile_match_gym_amd.shard import synthetic_actions
+    from tile_match_gym_amd.vec_env import TileMatchVecEnv, load_state
+    n, R, C, k, sm = 2048, 10, 10, 4, 14
+    cl, co = _lists(sm)
+    env = TileMatchVecEnv(n, R, C, k, 15, cl, co, seed=21, device=DEV, groups=2)
+    acts = synthetic_actions(range(n), 60, env.num_actions)
+    dacts = torch.from_numpy(acts).to(DEV)
+    env.reset()
+    for t in range(23):
+        env.step_raw(dacts[t])
+    p = tmp_path / "ck.npz"
+    env.save(p)
+    arrays, cfg = load_state(p)
+    assert ((arrays["rng"][:, 4] >> np.uint64(32)) & np.uint64(1)).any(), "some env should hold a buffered half-word"
+    o = orc.OracleBatch(R, C, k, sm, 15, arrays["rng"].copy(), threads=16)
+    o.board[:] = arrays["board"]
+    o.timer[:] = arrays["timer"]
+    o.eff[:] = arrays["eff"]
+    env2 = TileMatchVecEnv.load(p, device=DEV)
+    for t in range(23, 58):
+        env2.step(dacts[t])
+        o.step(acts[t], autoreset=True)
+        assert np.array_equal(env2.board.cpu().numpy(), o.board), t
+        assert np.array_equal(env2.rng_words(), o.rng), t
+        assert np.array_equal(env2.timer.cpu().numpy(), o.timer), t
+        assert np.array_equal(env2.reward.cpu().numpy(), o.reward), t
+        assert np.array_equal(env2.flags.cpu().numpy(), o.flags), t
+        assert np.array_equal(env2.eff.cpu().numpy().view(np.uint64), o.eff), t

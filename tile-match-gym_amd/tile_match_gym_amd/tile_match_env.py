@@ -43,19 +43,47 @@ def action_to_coords(num_rows: int, num_cols: int):
 
 
 class Board:
-    """Host view of the device board (mirror of board.py:41-93's public fields)."""
+    """The reference's Board (board.py:41-93) as a host mirror of one device
+    board: same constructor and public fields (`board` int32 [2,R,C],
+    `np_random`, `specials`, `action_to_coords`, ...), and the transition
+    entry points the reference's callers and tests use, run by the HIP kernels
+    on a batch of one:
 
-    def __init__(self, env: "TileMatchEnv", num_rows, num_cols, num_colours, colourless_specials, colour_specials):
-        self._env = env
+    * `generate_board()` (board.py:95-131) -> tmg_reset,
+    * `move(coord1, coord2)` (board.py:330-395) -> tmg_step with an untrusted
+      mask (the exact effectiveness test), returning the same 5-tuple,
+    * `possible_move()` (board.py:558-569) / `is_move_effective(board, c1, c2)`
+      (module level, board.py:735-787) -> tmg_effective.
+
+    `board` and the RNG position are uploaded before and downloaded after
+    every call, so hand edits of `board.board` behave as with the reference.
+    The order of coord1 / coord2 does not change the reference's result
+    (swap_coords and combination_match are symmetric in them), so a move is
+    replayed as the action of the table (board.py:77-93) holding that pair."""
+
+    def __init__(self, num_rows, num_cols, num_colours, colourless_specials=("cookie",),
+                 colour_specials=("vertical_laser", "horizontal_laser", "bomb"), np_random=None, board=None,
+                 device=None, _env=None):
         self.num_rows, self.num_cols, self.num_colours = num_rows, num_cols, num_colours
-        self.flat_size = num_rows * num_cols
-        self.colourless_specials = colourless_specials
-        self.colour_specials = colour_specials
-        self.specials = set(list(colourless_specials) + list(colour_specials))
-        self.num_actions = 2 * num_rows * num_cols - num_rows - num_cols
-        self.action_to_coords = action_to_coords(num_rows, num_cols)
-        self.board = np.ones((2, num_rows, num_cols), dtype=np.int32)
-        self.rng_words = np.zeros(5, dtype=np.uint64)
+        self.colourless_specials = list(colourless_specials)
+        self.colour_specials = list(colour_specials)
+        self.specials = set(self.colourless_specials + self.colour_specials)
+        self.rng_words = rng_words_from_generator(np_random if np_random is not None else np.random.default_rng(0))
+        if board is not None:                                                # board.py:64-74
+            board = np.array(board, dtype=np.int32) if isinstance(board, list) else board
+            self.board = np.array([board, np.ones_like(board)]) if len(board.shape) < 3 else board
+            self.num_rows, self.num_cols = self.board.shape[1], self.board.shape[2]
+        else:
+            self.board = np.ones((2, self.num_rows, self.num_cols), dtype=np.int32)
+        self.flat_size = int(self.num_rows * self.num_cols)
+        self.num_actions = int(2 * self.num_rows * self.num_cols - self.num_rows - self.num_cols)
+        self.action_to_coords = action_to_coords(self.num_rows, self.num_cols)
+        self._coord_to_action = {c: a for a, c in enumerate(self.action_to_coords)}
+        self._env = _env
+        self._device = device
+        self._dev = None                       # lazily: context + device buffers of a batch of one
+        self.num_specials_activated = 0
+        self.num_new_specials = 0
 
     @property
     def np_random(self) -> np.random.Generator:
@@ -64,6 +92,115 @@ class Board:
     @np_random.setter
     def np_random(self, gen):
         self.rng_words = rng_words_from_generator(gen)
+
+    # ----------------------------------------------------------- device side
+    def _buffers(self):
+        if self._dev is None:
+            dev = self._device
+            if dev is None:
+                if not torch.cuda.is_available():
+                    raise _native.TmgError("Board needs a HIP device (no CPU fallback)")
+                dev = torch.device("cuda", torch.cuda.current_device())
+            dev = torch.device(dev)
+            R, C = self.num_rows, self.num_cols
+            smask = _native.specials_mask(self.colourless_specials, self.colour_specials)
+            ctx = _native.Context(dev.index if dev.index is not None else 0, R, C, self.num_colours, smask, 1 << 30)
+            kw = dict(device=dev)
+            self._dev = dict(dev=dev, ctx=ctx, board=torch.zeros((1, 2, R, C), dtype=torch.int8, **kw),
+                             rng=torch.zeros((1, 5), dtype=torch.int64, **kw),
+                             timer=torch.zeros(1, dtype=torch.int32, **kw),
+                             eff=torch.zeros((1, ctx.mask_words), dtype=torch.int64, **kw),
+                             out=torch.zeros((3, 1), dtype=torch.int32, **kw),
+                             flags=torch.zeros(1, dtype=torch.uint8, **kw),
+                             act=torch.zeros(1, dtype=torch.int32, **kw))
+        return self._dev
+
+    def _stream(self, d):
+        return torch.cuda.current_stream(d["dev"]).cuda_stream
+
+    def _upload(self, d):
+        b = self.board
+        if b.shape != (2, self.num_rows, self.num_cols):
+            raise ValueError("board has the wrong shape")
+        d["board"].copy_(torch.from_numpy(np.ascontiguousarray(b, dtype=np.int8)).unsqueeze(0))
+        d["rng"].copy_(torch.from_numpy(self.rng_words.view(np.int64)).unsqueeze(0))
+
+    def _download(self, d):
+        self.board = d["board"][0].to(torch.int32).cpu().numpy()
+        self.rng_words = d["rng"][0].cpu().numpy().view(np.uint64).copy()
+
+    # -------------------------------------------------------------- methods
+    def generate_board(self):                                                # board.py:95-109
+        d = self._buffers()
+        self._upload(d)
+        d["ctx"].reset(1, d["board"].data_ptr(), d["rng"].data_ptr(), d["timer"].data_ptr(), d["eff"].data_ptr(),
+                       None, self._stream(d))
+        self._download(d)
+
+    def is_move_legal(self, coord1, coord2) -> bool:                         # board.py:242-267
+        (r1, c1), (r2, c2) = coord1, coord2
+        if not (0 <= r1 < self.num_rows and 0 <= c1 < self.num_cols):
+            return False
+        if not (0 <= r2 < self.num_rows and 0 <= c2 < self.num_cols):
+            return False
+        if (r1, c1) == (r2, c2):
+            return False
+        return (r1 == r2 or c1 == c2) and abs(r1 - r2) <= 1 and abs(c1 - c2) <= 1
+
+    def move(self, coord1, coord2):                                          # board.py:330-395
+        self.num_specials_activated = 0
+        self.num_new_specials = 0
+        if not self.is_move_legal(coord1, coord2):
+            raise ValueError(f"Invalid move: {coord1}, {coord2}")
+        key = (tuple(int(x) for x in coord1), tuple(int(x) for x in coord2))
+        a = self._coord_to_action.get(key)
+        if a is None:
+            a = self._coord_to_action[(key[1], key[0])]
+        d = self._buffers()
+        self._upload(d)
+        d["timer"].zero_()
+        d["act"].fill_(a)
+        out = d["out"]
+        d["ctx"].step(1, d["board"].data_ptr(), d["rng"].data_ptr(), d["timer"].data_ptr(), d["act"].data_ptr(),
+                      out[0].data_ptr(), out[1].data_ptr(), out[2].data_ptr(), d["flags"].data_ptr(),
+                      d["eff"].data_ptr(), 0, 0, self._stream(d))
+        self._download(d)
+        o = out[:, 0].cpu().numpy()
+        flags = int(d["flags"][0].item())
+        if flags & (_native.FLAG_ERROR | _native.FLAG_OVERFLOW):
+            raise _native.TmgError("device reported an error for this move")
+        self.num_new_specials, self.num_specials_activated = int(o[1]), int(o[2])
+        return (int(o[0]), bool(flags & _native.FLAG_COMBO), self.num_new_specials, self.num_specials_activated,
+                bool(flags & _native.FLAG_SHUFFLED))
+
+    def effective_actions(self) -> List[int]:
+        """Ascending actions a with is_move_effective(board, *action_to_coords[a])."""
+        d = self._buffers()
+        self._upload(d)
+        d["ctx"].effective(1, d["board"].data_ptr(), d["eff"].data_ptr(), self._stream(d))
+        w = d["eff"][0].cpu().numpy().view(np.uint64)
+        bits = np.unpackbits(w.view(np.uint8), bitorder="little")[:self.num_actions]
+        return [int(a) for a in np.nonzero(bits)[0]]
+
+    def possible_move(self, grid=None) -> bool:                              # board.py:558-569
+        if grid is None:
+            return bool(self.effective_actions())
+        return bool(Board(self.num_rows, self.num_cols, self.num_colours, self.colourless_specials,
+                          self.colour_specials, board=np.asarray(grid), device=self._device).effective_actions())
+
+
+def is_move_effective(board, coord1, coord2) -> bool:
+    """board.py:735-787 on the device (effective_kernel) for one board and one
+    pair of adjacent coords.  The board may hold any colours / types; the
+    answer does not depend on the colour count or the enabled specials."""
+    b = np.asarray(board)
+    R, C = b.shape[1], b.shape[2]
+    bd = Board(R, C, 4, [], [], board=b)
+    key = (tuple(int(x) for x in coord1), tuple(int(x) for x in coord2))
+    a = bd._coord_to_action.get(key)
+    if a is None:
+        a = bd._coord_to_action[(key[1], key[0])]
+    return a in bd.effective_actions()
 
 
 class TileMatchEnv(_EnvBase):
@@ -94,7 +231,8 @@ class TileMatchEnv(_EnvBase):
         smask = _native.specials_mask(colourless_specials, colour_specials)
         self._ctx = _native.Context(self.device.index if self.device.index is not None else 0,
                                     num_rows, num_cols, num_colours, smask, num_moves)
-        self.board = Board(self, num_rows, num_cols, num_colours, colourless_specials, colour_specials)
+        self.board = Board(num_rows, num_cols, num_colours, colourless_specials, colour_specials,
+                           device=self.device, _env=self)
         self.board.rng_words = rng_words_from_seed(seed)                     # tile_match_env.py:49
         R, C = num_rows, num_cols
         obs_low = np.array([np.zeros((R, C), dtype=np.int32),
