@@ -1678,7 +1678,7 @@ __global__ __launch_bounds__(64 * TMG_WPB, MAXN > 128 ? TMG_RESET512_WAVES : 1) 
     const LaneJump J = load_jump(P, lane, g);
     const Cells<MAXN / 64> cl = make_cells<MAXN / 64>(P, lane);
     int fl;
-    if constexpr (SBNB > 0) fl = sb_generate<SBNB, CODD>(P, w, lane, J, g, cl);   // board.py:95-109
+    if constexpr (SBNB > 0) fl = sb_generate<SBNB, CODD, TMG_SB_VDET != 0>(P, w, lane, J, g, cl);   // board.py:95-109
     else fl = generate_board(P, w, lane, J, g, cl);
     note_status(P, lane, fl ? ST_INTERNAL : 0u);
     store_board(P, w, lane, board + e * 2 * N);

@@ -42,6 +42,7 @@ inline int emu_update_dpp(int old, int src, int ctrl, int row_mask, int bank_mas
 // the builtin returns int (an OR into a 64-bit value sign-extends it, as on the device)
 #define __builtin_amdgcn_readlane(v, l) ((int)emu_readlane((uint32_t)(v), (l)))
 #define __builtin_amdgcn_readfirstlane(v) ((int)emu_readlane((uint32_t)(v), 0))
+#define __builtin_amdgcn_ds_bpermute(a, v) ((int)emu_readlane((uint32_t)(v), ((a) >> 2) & 63))
 #define __builtin_amdgcn_fence(order, scope) emu_sync()
 #define __builtin_amdgcn_wave_barrier() ((void)0)
 inline void __syncthreads() { emu_sync(); }
