@@ -47,6 +47,9 @@ namespace tmg {
 #define TMG_XCD 1          // XCD-aware workgroup -> env mapping
 #endif
 
+#ifndef TMG_LEAN_DEFER
+#define TMG_LEAN_DEFER 0       // 1: 128-cell lean step kernels autoreset by a masked reset launch (A/B: -1 %)
+#endif
 #ifndef TMG_STATUS
 #define TMG_STATUS 1           // 0: no sticky status word (A/B of its cost only; tmg_status then reads 0)
 #endif
@@ -432,19 +435,28 @@ __host__ __device__ __forceinline__ void action_coords(int R, int C, int a, int 
 // per-lane cell coordinates of each 64-cell pass, computed once per kernel
 template <int NP>
 struct Cells {
-    int r[NP], c[NP];
-    uint32_t vbad[NP], hbad[NP];   // 0 iff a vertical / horizontal triple can be anchored here
+    // per 64-cell pass, one word per lane: key base ((r << 8) | (255 - c)) << 1
+    // in bits 0..14 (the first-line key of remove_colour_lines' search), vbad
+    // in bit 15, hbad in bit 16 (0 iff a vertical / horizontal triple can be
+    // anchored here).  One VGPR per pass instead of four (the 512-cell
+    // kernels are VGPR-bound).
+    uint32_t pk[NP];
+    __device__ __forceinline__ int key(int i) const { return (int)(pk[i] & 0x7fffu); }
+    __device__ __forceinline__ int r(int i) const { return (int)((pk[i] >> 9) & 63u); }
+    __device__ __forceinline__ int c(int i) const { return 255 - (int)((pk[i] >> 1) & 255u); }
+    __device__ __forceinline__ uint32_t vbad(int i) const { return (pk[i] >> 15) & 1u; }
+    __device__ __forceinline__ uint32_t hbad(int i) const { return (pk[i] >> 16) & 1u; }
 };
 template <int NP>
 __device__ __forceinline__ Cells<NP> make_cells(const Params &P, int lane) {
     Cells<NP> cl;
 #pragma unroll
     for (int i = 0; i < NP; i++) {
-        int p = i * 64 + lane;
-        cl.r[i] = div_c(P, p);
-        cl.c[i] = p - cl.r[i] * P.C;
-        cl.vbad[i] = (p < P.N && cl.r[i] >= 2) ? 0u : 1u;
-        cl.hbad[i] = (p < P.N && cl.c[i] + 2 < P.C) ? 0u : 1u;
+        const int p = i * 64 + lane;
+        const int r = div_c(P, p), c = p - r * P.C;
+        const uint32_t vbad = (p < P.N && r >= 2) ? 0u : 1u;
+        const uint32_t hbad = (p < P.N && c + 2 < P.C) ? 0u : 1u;
+        cl.pk[i] = ((uint32_t)(((r & 63) << 8) | (255 - (c & 255))) << 1) | (vbad << 15) | (hbad << 16);
     }
     return cl;
 }
@@ -614,7 +626,7 @@ __device__ __forceinline__ bool scan_effective(const Params &P, WS &w, int lane,
         for (int i = 0; i < WS::NP; i++) {
             int p = i * 64 + lane;
             if (p < N) {
-                int r = cl.r[i], c = cl.c[i], x = col[p];
+                int r = cl.r(i), c = cl.c(i), x = col[p];
                 odd |= typ[p] < 0;
                 odd |= (c + 2 < C) && col[p + 1] == x && col[p + 2] == x && typ[p + 2] >= 0;
                 odd |= (r + 2 < R) && col[p + C] == x && col[p + 2 * C] == x && typ[p + 2 * C] >= 0;
@@ -670,8 +682,8 @@ __device__ __forceinline__ int detect(const Params &P, const WS &w, int lane, co
         const int u1 = col[max(pc - C, 0)], u2 = col[max(pc - 2 * C, 0)];
         const int h1 = col[min(pc + 1, N1)], h2 = col[min(pc + 2, N1)];
         const uint32_t tbad = (uint32_t)((int)typ[pc] - 1) >> 31;            // 1 iff type <= 0
-        const uint32_t vb = cl.vbad[i] | tbad | ne(u1, x) | ne(u2, x);
-        const uint32_t hb = cl.hbad[i] | tbad | ne(h1, x) | ne(h2, x);
+        const uint32_t vb = cl.vbad(i) | tbad | ne(u1, x) | ne(u2, x);
+        const uint32_t hb = cl.hbad(i) | tbad | ne(h1, x) | ne(h2, x);
         d.v[i] = __ballot(vb == 0);
         d.h[i] = __ballot(hb == 0);
         const uint64_t m = d.v[i] | d.h[i];
@@ -701,27 +713,51 @@ __device__ __forceinline__ int run_top(const Params &P, const WS &w, int lane, i
 // one holding row lim's last cell upwards and the scan stops one pass above
 // the first pass holding an anchor: the bottom-most anchor row (C <= 64
 // cells) lies in that pass and the one above it.  ra: the anchor row found.
-template <class WS>
+template <bool ROLL, class WS>
 __device__ __forceinline__ int first_line_row(const Params &P, const WS &w, int lane, const Cells<WS::NP> &cl,
                                               int lim, int &ra) {
     const int C = P.C, N = P.N, N1 = P.N - 1;
     const int8_t *col = w.brd, *typ = w.brd + N;
     const int last = min((lim + 1) * C, N) - 1;          // highest cell that may anchor a line
     int best = -1, stop = -2;                            // stop: lowest pass still to scan, once found
+    if constexpr (!ROLL || WS::NP <= 2) {
 #pragma unroll
-    for (int i = WS::NP - 1; i >= 0; i--) {
-        if (i * 64 > last || i < stop) continue;         // wave-uniform
-        const int p = i * 64 + lane;
-        const int pc = min(p, N1);
-        const int x = col[pc];
-        const int u1 = col[max(pc - C, 0)], u2 = col[max(pc - 2 * C, 0)];
-        const int h1 = col[min(pc + 1, N1)], h2 = col[min(pc + 2, N1)];
-        const uint32_t tbad = (uint32_t)((int)typ[pc] - 1) >> 31;
-        const uint32_t vb = cl.vbad[i] | tbad | ne(u1, x) | ne(u2, x);
-        const uint32_t hb = cl.hbad[i] | tbad | ne(h1, x) | ne(h2, x);
-        const int base = ((cl.r[i] << 8) | (255 - cl.c[i])) << 1;
-        best = max(best, max(vb == 0 ? base | 1 : -1, hb == 0 ? base : -1));
-        if (stop == -2 && __ballot(best >= 0) != 0ULL) stop = i - 1;
+        for (int i = WS::NP - 1; i >= 0; i--) {
+            if (i * 64 > last || i < stop) continue;     // wave-uniform
+            const int p = i * 64 + lane;
+            const int pc = min(p, N1);
+            const int x = col[pc];
+            const int u1 = col[max(pc - C, 0)], u2 = col[max(pc - 2 * C, 0)];
+            const int h1 = col[min(pc + 1, N1)], h2 = col[min(pc + 2, N1)];
+            const uint32_t tbad = (uint32_t)((int)typ[pc] - 1) >> 31;
+            const uint32_t vb = cl.vbad(i) | tbad | ne(u1, x) | ne(u2, x);
+            const uint32_t hb = cl.hbad(i) | tbad | ne(h1, x) | ne(h2, x);
+            const int base = cl.key(i);
+            best = max(best, max(vb == 0 ? base | 1 : -1, hb == 0 ? base : -1));
+            if (stop == -2 && __ballot(best >= 0) != 0ULL) stop = i - 1;
+        }
+    } else {
+        // ROLL (512-cell step kernels): a rolled loop from the pass holding
+        // `last` down to the stop pass, the cell's row / column recomputed per
+        // pass.  The unrolled scan keeps eight passes' loads and cells live:
+        // 187 -> 166 VGPRs, 2 -> 3 waves/SIMD for the step kernel; the reset
+        // kernel keeps the unrolled form (its loads overlap: faster there).
+        (void)cl;
+        for (int i = last >> 6; i >= 0 && i >= stop; i--) {
+            const int p = i * 64 + lane;
+            const int pc = min(p, N1);
+            const int r = div_c(P, p), c = p - r * C;
+            const int x = col[pc];
+            const int u1 = col[max(pc - C, 0)], u2 = col[max(pc - 2 * C, 0)];
+            const int h1 = col[min(pc + 1, N1)], h2 = col[min(pc + 2, N1)];
+            const uint32_t tbad = (uint32_t)((int)typ[pc] - 1) >> 31;
+            const uint32_t vbad = (p < N && r >= 2) ? 0u : 1u, hbad = (p < N && c + 2 < C) ? 0u : 1u;
+            const uint32_t vb = vbad | tbad | ne(u1, x) | ne(u2, x);
+            const uint32_t hb = hbad | tbad | ne(h1, x) | ne(h2, x);
+            const int base = (((r & 63) << 8) | (255 - (c & 255))) << 1;
+            best = max(best, max(vb == 0 ? base | 1 : -1, hb == 0 ? base : -1));
+            if (stop == -2 && __ballot(best >= 0) != 0ULL) stop = i - 1;
+        }
     }
     if (stop == -2) return -1;
     const int key = wave_max(best);
@@ -824,7 +860,7 @@ __device__ __forceinline__ void shuffle(const Params &P, WS &w, int lane, Rng &g
 // (board.py:102-109, 381-391, remove_colour_lines :120-131).  Leaves the final
 // board's effective mask in w.effw.  Returns FL_SHUF when a shuffle ran, FL_ERR
 // when the shuffle cap ended the loop.
-template <class WS>
+template <bool ROLL = true, class WS>
 __device__ __forceinline__ int ensure_playable(const Params &P, WS &w, int lane, const LaneJump &J, Rng &g,
                                 const Cells<WS::NP> &cl) {
     int fl = 0;
@@ -834,7 +870,7 @@ __device__ __forceinline__ int ensure_playable(const Params &P, WS &w, int lane,
         int lim = P.R - 1;
         for (;;) {
             int ra = 0;
-            int r0 = first_line_row(P, w, lane, cl, lim, ra);
+            int r0 = first_line_row<ROLL>(P, w, lane, cl, lim, ra);
             if (r0 < 0) break;
             int row = P.R - 1 < r0 + 1 ? P.R - 1 : r0 + 1;   // colour plane only, rows 0..row
             draw_colours(P, lane, J, g, (row + 1) * P.C, w.brd, w.trash);
@@ -852,13 +888,13 @@ __device__ __forceinline__ int ensure_playable(const Params &P, WS &w, int lane,
 }
 
 // generate_board, board.py:95-109; returns FL_ERR when a safety cap was hit
-template <class WS>
+template <bool ROLL = true, class WS>
 __device__ __forceinline__ int generate_board(const Params &P, WS &w, int lane, const LaneJump &J, Rng &g, const Cells<WS::NP> &cl) {
     const int N = P.N;
     draw_colours(P, lane, J, g, N, w.brd, w.trash);
     for (int p = lane; p < N; p += 64) w.brd[N + p] = 1;
     WSYNC();
-    return ensure_playable(P, w, lane, J, g, cl) & FL_ERR;
+    return ensure_playable<ROLL>(P, w, lane, J, g, cl) & FL_ERR;
 }
 
 // Queue env e for spill_kernel; false when the queue is full.
@@ -1505,6 +1541,9 @@ __device__ __forceinline__ uint32_t step_env(
     int32_t *__restrict__ n_act, uint8_t *__restrict__ flags_out, uint64_t *__restrict__ eff, int trust_eff,
     int autoreset, L *lists) {
     const int N = P.N, W = P.W;
+    // the 128-cell lean kernels leave autoresets to a reset_kernel launch
+    // (TMG_LEAN_DEFER): no generate_board code in the hot step kernel
+    constexpr bool LEAN_DEFER = TMG_LEAN_DEFER && !GEN && MAXN == 128 && !SPILL;
     STAMP(e, 0);
     const int a = __builtin_amdgcn_readfirstlane(actions[e]);             // wave-uniform loads
     const int t0 = __builtin_amdgcn_readfirstlane(timer[e]);
@@ -1519,9 +1558,13 @@ __device__ __forceinline__ uint32_t step_env(
     int flags = done ? FL_DONE : 0;
     bool effective = false;
     if (trust_eff) effective = (bcast64(ge[a >> 6]) >> (a & 63)) & 1ULL;    // board.py:352 via cached mask
-    if (trust_eff && !effective && !(done && autoreset)) {                  // no state change at all
-        if (done) for (int i = lane; i < W; i += 64) ge[i] = 0ULL;          // tile_match_env.py:119-120
-        if (lane == 0) { timer[e] = t1; reward[e] = 0; n_new[e] = 0; n_act[e] = 0; flags_out[e] = (uint8_t)flags; }
+    if (trust_eff && !effective && !(done && autoreset == 1)) {             // no state change at all
+        const bool defer = done && autoreset;                               // autoreset == 2: reset_kernel next
+        if (done && !defer) for (int i = lane; i < W; i += 64) ge[i] = 0ULL; // tile_match_env.py:119-120
+        if (lane == 0) {
+            timer[e] = defer ? 0 : t1; reward[e] = 0; n_new[e] = 0; n_act[e] = 0;
+            flags_out[e] = (uint8_t)(flags | (defer ? FL_RESET : 0));
+        }
         STAMP(e, 7);
         return 0;
     }
@@ -1566,10 +1609,12 @@ __device__ __forceinline__ uint32_t step_env(
     STAMP(e, 4);
     int tnew = t1;
     if (done && autoreset) {                                                // reset() without a seed
-        if (autoreset == 1) {
-            if constexpr (SBNB > 0) flags |= sb_generate<SBNB, CODD>(P, w, lane, J, g, cl);
-            else flags |= generate_board(P, w, lane, J, g, cl);
-            changed = true;
+        if constexpr (!LEAN_DEFER) {
+            if (autoreset == 1) {
+                if constexpr (SBNB > 0) flags |= sb_generate<SBNB, CODD>(P, w, lane, J, g, cl);
+                else flags |= generate_board(P, w, lane, J, g, cl);
+                changed = true;
+            }
         }                                      // autoreset == 2: reset_kernel regenerates FL_RESET envs next
         tnew = 0;
         flags |= FL_RESET;
@@ -1679,7 +1724,7 @@ __global__ __launch_bounds__(64 * TMG_WPB, MAXN > 128 ? TMG_RESET512_WAVES : 1) 
     const Cells<MAXN / 64> cl = make_cells<MAXN / 64>(P, lane);
     int fl;
     if constexpr (SBNB > 0) fl = sb_generate<SBNB, CODD, TMG_SB_VDET != 0>(P, w, lane, J, g, cl);   // board.py:95-109
-    else fl = generate_board(P, w, lane, J, g, cl);
+    else fl = generate_board<false>(P, w, lane, J, g, cl);
     note_status(P, lane, fl ? ST_INTERNAL : 0u);
     store_board(P, w, lane, board + e * 2 * N);
     store_rng(rng + e * 5, g, lane);

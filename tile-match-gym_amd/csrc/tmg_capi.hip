@@ -165,7 +165,7 @@ static int do_step(tmg_ctx *ctx, Params P, StepArgs a, hipStream_t s) {
     }
     const dim3 grid = env_grid(a.n);
     a.autoreset = a.autoreset ? 1 : 0;
-    const int deferred = a.autoreset && (ctx->maxn == 512 || (ctx->defer_general && !lean));
+    const int deferred = a.autoreset && (ctx->maxn == 512 || (ctx->defer_general && !lean) || (TMG_LEAN_DEFER && lean));
     // 512-cell kernels (and, with defer_general, the 128-cell general one):
     // finished boards are regenerated by a reset_kernel launch masked by
     // FL_RESET, which runs at several times the step kernel's occupancy

@@ -300,7 +300,12 @@ int emu_step(int R, int C, int k, int smask, int moves, int64_t n, int8_t *board
     S.autoreset = autoreset ? 1 : 0;
     if (P.N <= 128) {
         if (sb_ok(P)) {
-            if (lean) { if (P.C & 1) emu_step_sb<false, true>(S); else emu_step_sb<false, false>(S); }
+            if (lean) {
+                const int deferred = TMG_LEAN_DEFER ? S.autoreset : 0;    // as tmg_capi.hip's do_step
+                if (deferred) S.autoreset = 2;
+                if (P.C & 1) emu_step_sb<false, true>(S); else emu_step_sb<false, false>(S);
+                if (deferred) emu_do_reset(P, n, board, rng, timer, eff, flags, tmg::FL_RESET);
+            }
             else {
                 // general kernel: autoreset deferred to a FL_RESET-masked reset, as tmg_capi.hip
                 const int deferred = S.autoreset;
@@ -310,7 +315,10 @@ int emu_step(int R, int C, int k, int smask, int moves, int64_t n, int8_t *board
                 if (deferred) emu_do_reset(P, n, board, rng, timer, eff, flags, tmg::FL_RESET);
             }
         } else if (lean) {
+            const int deferred = TMG_LEAN_DEFER ? S.autoreset : 0;
+            if (deferred) S.autoreset = 2;
             emu_step_kernel<128, false, 0, false>(S);
+            if (deferred) emu_do_reset(P, n, board, rng, timer, eff, flags, tmg::FL_RESET);
         } else {
             emu_step_kernel<128, true, 0, false>(S);
             emu_spill<128>(S);
