@@ -56,6 +56,9 @@ namespace tmg {
 #ifndef TMG_GEN128_WAVES
 #define TMG_GEN128_WAVES 4     // min waves per SIMD for the 128-cell general step kernel (caps it at 128 VGPRs)
 #endif
+#ifndef TMG_RQ128_WAVES
+#define TMG_RQ128_WAVES 5      // min waves per SIMD for the 128-cell reset-queue kernel (87 VGPRs, no spill)
+#endif
 #ifndef TMG_RESET512_WAVES
 #define TMG_RESET512_WAVES 4   // min waves per SIMD for the 512-cell reset kernel (caps its VGPRs)
 #endif
@@ -99,6 +102,14 @@ struct SpillQ {
     int64_t env[TMG_SPILL_CAP];
 };
 
+// Per-stream queue of the envs a deferred-autoreset step finished (step_env
+// with autoreset == 2), drained by reset_queue_kernel.  Sized by the host for
+// the launch's env count.
+struct ResetQ {
+    uint32_t count, next, done, pad;   // queued envs; next to take; waves finished
+    int64_t env[1];                    // [capacity]
+};
+
 struct Params {
     int R, C, N, A, W, k, smask, num_moves;
     uint32_t thr;                 // Lemire threshold (2^32 - k) % k; 0 for powers of two
@@ -118,6 +129,7 @@ struct Params {
     uint32_t oh_sel;              // type ids of the special channels, int8 each (wrappers.py:37-46)
     SpillQ *spill;                // this launch's stream's spill queue (general kernels)
     void *spill_ws;               // TMG_SPILL_WAVES WsSerialBig<MAXN> for spill_kernel
+    ResetQ *resetq;               // deferred autoresets go here (null: FL_RESET-masked reset launch)
 };
 
 // host: the per-row masks of Params::sb_rows (boards of <= 128 cells)
@@ -149,6 +161,7 @@ inline Params make_params(int R, int C, int k, int smask, int num_moves, const u
     P.status = nullptr;
     P.spill = nullptr;
     P.spill_ws = nullptr;
+    P.resetq = nullptr;
     P.oh = nullptr;
     P.oh_dtype = P.oh_ch = P.oh_nsel = 0;
     P.oh_sel = 0;
@@ -1564,6 +1577,7 @@ __device__ __forceinline__ uint32_t step_env(
         if (lane == 0) {
             timer[e] = defer ? 0 : t1; reward[e] = 0; n_new[e] = 0; n_act[e] = 0;
             flags_out[e] = (uint8_t)(flags | (defer ? FL_RESET : 0));
+            if (defer && P.resetq) P.resetq->env[atomicAdd(&P.resetq->count, 1u)] = e;
         }
         STAMP(e, 7);
         return 0;
@@ -1618,6 +1632,7 @@ __device__ __forceinline__ uint32_t step_env(
         }                                      // autoreset == 2: reset_kernel regenerates FL_RESET envs next
         tnew = 0;
         flags |= FL_RESET;
+        if (autoreset == 2 && lane == 0 && P.resetq) P.resetq->env[atomicAdd(&P.resetq->count, 1u)] = e;
     }
     STAMP(e, 5);
     if (changed) {
@@ -1704,20 +1719,11 @@ __global__ __launch_bounds__(64) void spill_kernel(
     }
 }
 
-// TileMatchEnv.reset without a seed (tile_match_env.py:84-91)
-template <int MAXN, int SBNB = 0, bool CODD = false>
-__global__ __launch_bounds__(64 * TMG_WPB, MAXN > 128 ? TMG_RESET512_WAVES : 1) void reset_kernel(Params P, int64_t n, int8_t *__restrict__ board,
-                                                             uint64_t *__restrict__ rng, int32_t *__restrict__ timer,
-                                                             uint64_t *__restrict__ eff,
-                                                             const uint8_t *__restrict__ env_mask, int mask_bits) {
-    TMG_SMEM_DECL(smem);
-    using WS = Ws<MAXN, false>;
-    const int lane = threadIdx.x & 63;
-    const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
-    WS &w = reinterpret_cast<WS *>(smem)[wv];
-    const int64_t e = wg_env0() + wv;
-    if (e >= n) return;
-    if (env_mask && !(__builtin_amdgcn_readfirstlane((int)env_mask[e]) & mask_bits)) return;
+// TileMatchEnv.reset without a seed (tile_match_env.py:84-91) of env e
+template <int MAXN, int SBNB, bool CODD, class WS>
+__device__ __forceinline__ void reset_env(const Params &P, WS &w, int lane, int64_t e, int8_t *__restrict__ board,
+                                          uint64_t *__restrict__ rng, int32_t *__restrict__ timer,
+                                          uint64_t *__restrict__ eff) {
     const int N = P.N, W = P.W;
     Rng g = load_rng(rng + e * 5);
     const LaneJump J = load_jump(P, lane, g);
@@ -1731,6 +1737,50 @@ __global__ __launch_bounds__(64 * TMG_WPB, MAXN > 128 ? TMG_RESET512_WAVES : 1) 
     if (P.oh) store_onehot(P, w, lane, e);
     for (int i = lane; i < W; i += 64) eff[e * W + i] = w.effw[i];
     if (lane == 0) timer[e] = 0;
+}
+
+template <int MAXN, int SBNB = 0, bool CODD = false>
+__global__ __launch_bounds__(64 * TMG_WPB, MAXN > 128 ? TMG_RESET512_WAVES : 1) void reset_kernel(Params P, int64_t n, int8_t *__restrict__ board,
+                                                             uint64_t *__restrict__ rng, int32_t *__restrict__ timer,
+                                                             uint64_t *__restrict__ eff,
+                                                             const uint8_t *__restrict__ env_mask, int mask_bits) {
+    TMG_SMEM_DECL(smem);
+    using WS = Ws<MAXN, false>;
+    const int lane = threadIdx.x & 63;
+    const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    WS &w = reinterpret_cast<WS *>(smem)[wv];
+    const int64_t e = wg_env0() + wv;
+    if (e >= n) return;
+    if (env_mask && !(__builtin_amdgcn_readfirstlane((int)env_mask[e]) & mask_bits)) return;
+    reset_env<MAXN, SBNB, CODD>(P, w, lane, e, board, rng, timer, eff);
+}
+
+// The deferred autoresets of one step launch: the envs its step kernel queued
+// (P.resetq), drained by a fixed grid of one-wave workgroups.  Workgroup b
+// takes entry b first, then, while entries remain, the next untaken one
+// (q->next, counting from the grid size): no atomic at all when the queue
+// holds at most one entry per workgroup (a step where few episodes end), and
+// the long regenerations of a storm spread over the grid as waves free up.
+// Every lane takes part in the fetch (lane 0 adds 1, the others 0), so the
+// loop exit stays wave-uniform.  The host zeroes the queue after the launch.
+template <int MAXN, int SBNB = 0, bool CODD = false>
+__global__ __launch_bounds__(64, MAXN > 128 ? TMG_RESET512_WAVES : TMG_RQ128_WAVES) void reset_queue_kernel(
+    Params P, int8_t *__restrict__ board, uint64_t *__restrict__ rng, int32_t *__restrict__ timer,
+    uint64_t *__restrict__ eff) {
+    TMG_SMEM_DECL(smem);
+    using WS = Ws<MAXN, false>;
+    const int lane = threadIdx.x & 63;
+    WS &w = *reinterpret_cast<WS *>(smem);
+    ResetQ *q = P.resetq;
+    const uint32_t cnt = (uint32_t)__builtin_amdgcn_readfirstlane((int)q->count);
+    uint32_t i = blockIdx.x;
+    while (i < cnt) {
+        const int64_t e = (int64_t)bcast64((uint64_t)q->env[i]);
+        WSYNC();
+        reset_env<MAXN, SBNB, CODD>(P, w, lane, e, board, rng, timer, eff);
+        if (cnt <= gridDim.x) break;
+        i = gridDim.x + (uint32_t)__builtin_amdgcn_readfirstlane((int)atomicAdd(&q->next, lane == 0 ? 1u : 0u));
+    }
 }
 
 // TileMatchEnv._get_effective_actions for arbitrary boards (tile_match_env.py:118-124)

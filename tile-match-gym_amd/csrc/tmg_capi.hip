@@ -43,9 +43,12 @@ struct tmg_ctx {
         hipStream_t stream;
         tmg::SpillQ *q;
         void *ws;
+        tmg::ResetQ *rq;     // deferred-autoreset queue of this stream
+        int64_t rq_cap;
     };
     std::vector<Spill> spills;
     int spill_launch;    // TMG_SPILL=0 skips the spill launches (cost A/B only: overflowing steps are then lost)
+    int reset_queue;     // deferred autoresets through a queue (TMG_RESETQ=1) instead of an FL_RESET-masked launch
 };
 
 using tmg::Params;
@@ -74,7 +77,7 @@ static int spill_for(tmg_ctx *ctx, hipStream_t s, tmg::SpillQ **q, void **ws) {
     for (const auto &x : ctx->spills)
         if (x.stream == s) { *q = x.q; *ws = x.ws; return 0; }
     const size_t wsz = ctx->maxn == 128 ? sizeof(tmg::WsSerialBig<128>) : sizeof(tmg::WsSerialBig<512>);
-    tmg_ctx::Spill sp{s, nullptr, nullptr};
+    tmg_ctx::Spill sp{s, nullptr, nullptr, nullptr, 0};
     int rc = hip_check(hipMalloc(&sp.q, sizeof(tmg::SpillQ)), "hipMalloc");
     if (!rc) rc = hip_check(hipMalloc(&sp.ws, wsz * TMG_SPILL_WAVES), "hipMalloc");
     // zeroed in order on s itself (a memset on the null stream is not ordered
@@ -89,6 +92,42 @@ static int spill_for(tmg_ctx *ctx, hipStream_t s, tmg::SpillQ **q, void **ws) {
     *q = sp.q;
     *ws = sp.ws;
     return 0;
+}
+
+// the stream's deferred-autoreset queue, holding at least n envs (zeroed on s)
+static int resetq_for(tmg_ctx *ctx, hipStream_t s, int64_t n, tmg::ResetQ **out) {
+    tmg_ctx::Spill *sp = nullptr;
+    for (auto &x : ctx->spills)
+        if (x.stream == s) sp = &x;
+    if (!sp) return fail(-5, "no spill entry for this stream");
+    if (sp->rq_cap < n) {
+        int rc = 0;
+        if (sp->rq) {                                  // grow: the old queue may still be in use on s
+            rc = hip_check(hipStreamSynchronize(s), "hipStreamSynchronize");
+            (void)hipFree(sp->rq);
+            sp->rq = nullptr;
+            sp->rq_cap = 0;
+        }
+        const size_t bytes = sizeof(tmg::ResetQ) + (size_t)n * sizeof(int64_t);
+        if (!rc) rc = hip_check(hipMalloc(&sp->rq, bytes), "hipMalloc");
+        if (!rc) rc = hip_check(hipMemsetAsync(sp->rq, 0, sizeof(tmg::ResetQ), s), "hipMemsetAsync");
+        if (rc) return rc;
+        sp->rq_cap = n;
+    }
+    *out = sp->rq;
+    return 0;
+}
+
+template <int MAXN, int NB, bool CODD>
+static void launch_reset_queue(hipStream_t s, const Params &P, int64_t n, int8_t *board, uint64_t *rng,
+                               int32_t *timer, uint64_t *eff) {
+    // a fixed grid of one-wave workgroups draining the queue: about the waves
+    // the chip holds at the kernel's occupancy (the queue holds <= n envs)
+    const int64_t full = MAXN > 128 ? 256 * 4 * TMG_RESET512_WAVES : 256 * 4 * TMG_RQ128_WAVES;
+    const unsigned g = (unsigned)(n < full ? n : full);
+    hipLaunchKernelGGL((tmg::reset_queue_kernel<MAXN, NB, CODD>), dim3(g), dim3(64), sizeof(tmg::Ws<MAXN, false>), s,
+                       P, board, rng, timer, eff);
+    (void)hipMemsetAsync(P.resetq, 0, 16, s);                // count / next / done for the next launch
 }
 
 template <int MAXN>
@@ -159,13 +198,14 @@ static int do_reset(tmg_ctx *ctx, const Params &P, int64_t n, int8_t *board, uin
 
 static int do_step(tmg_ctx *ctx, Params P, StepArgs a, hipStream_t s) {
     const bool lean = ctx->P.smask == 0 && a.trust_eff;
-    if (!lean) {                                   // general kernels: this stream's spill queue
-        int rc = spill_for(ctx, s, &P.spill, &P.spill_ws);
-        if (rc) return rc;
-    }
     const dim3 grid = env_grid(a.n);
     a.autoreset = a.autoreset ? 1 : 0;
     const int deferred = a.autoreset && (ctx->maxn == 512 || (ctx->defer_general && !lean) || (TMG_LEAN_DEFER && lean));
+    if (!lean || deferred) {                       // this stream's spill / deferred-reset queues
+        int rc = spill_for(ctx, s, &P.spill, &P.spill_ws);
+        if (!rc && deferred && ctx->reset_queue) rc = resetq_for(ctx, s, a.n, &P.resetq);
+        if (rc) return rc;
+    }
     // 512-cell kernels (and, with defer_general, the 128-cell general one):
     // finished boards are regenerated by a reset_kernel launch masked by
     // FL_RESET, which runs at several times the step kernel's occupancy
@@ -198,7 +238,25 @@ static int do_step(tmg_ctx *ctx, Params P, StepArgs a, hipStream_t s) {
         if (rc) return rc;
     }
     if (!deferred) return 0;
-    return do_reset(ctx, P, a.n, a.board, a.rng, a.timer, a.eff, a.flags, tmg::FL_RESET, s);
+    if (!P.resetq) return do_reset(ctx, P, a.n, a.board, a.rng, a.timer, a.eff, a.flags, tmg::FL_RESET, s);
+    if (ctx->maxn == 512) {
+        launch_reset_queue<512, 0, false>(s, P, a.n, a.board, a.rng, a.timer, a.eff);
+    } else if (ctx->sb) {
+        const bool codd = P.C & 1;
+        switch (tmg::sb_planes(P.k)) {
+        case 1: codd ? launch_reset_queue<128, 1, true>(s, P, a.n, a.board, a.rng, a.timer, a.eff)
+                     : launch_reset_queue<128, 1, false>(s, P, a.n, a.board, a.rng, a.timer, a.eff); break;
+        case 2: codd ? launch_reset_queue<128, 2, true>(s, P, a.n, a.board, a.rng, a.timer, a.eff)
+                     : launch_reset_queue<128, 2, false>(s, P, a.n, a.board, a.rng, a.timer, a.eff); break;
+        case 3: codd ? launch_reset_queue<128, 3, true>(s, P, a.n, a.board, a.rng, a.timer, a.eff)
+                     : launch_reset_queue<128, 3, false>(s, P, a.n, a.board, a.rng, a.timer, a.eff); break;
+        default: codd ? launch_reset_queue<128, 4, true>(s, P, a.n, a.board, a.rng, a.timer, a.eff)
+                      : launch_reset_queue<128, 4, false>(s, P, a.n, a.board, a.rng, a.timer, a.eff); break;
+        }
+    } else {
+        launch_reset_queue<128, 0, false>(s, P, a.n, a.board, a.rng, a.timer, a.eff);
+    }
+    return hip_check(hipGetLastError(), "kernel launch");
 }
 
 static int do_effective(tmg_ctx *ctx, int64_t n, const int8_t *board, uint64_t *eff, hipStream_t s) {
@@ -320,6 +378,13 @@ int tmg_create(tmg_ctx **out, int device, int rows, int cols, int colours, uint3
     c->defer_general = c->sb && !(denv && denv[0] == '0');
     const char *spenv = getenv("TMG_SPILL");
     c->spill_launch = !(spenv && spenv[0] == '0');
+    // TMG_RESETQ=1: deferred autoresets through the per-stream queue instead of
+    // the FL_RESET-masked launch.  Measured on c3: -54 us per normal step (no
+    // wave per env to dispatch) but +2.1 ms per reset storm (the looping queue
+    // kernel needs 87 VGPRs, 5 waves/SIMD, against the reset kernel's 69 / 7):
+    // -5 % overall, so off by default.
+    const char *rqenv = getenv("TMG_RESETQ");
+    c->reset_queue = rqenv && rqenv[0] == '1';
     uint64_t tab[64 * 4];
     tmg::build_jump_table(tab);
     rc = hip_check(hipMalloc(&c->d_jump, sizeof tab), "hipMalloc");
@@ -365,6 +430,7 @@ int tmg_destroy(tmg_ctx *ctx) {
     for (const auto &x : ctx->spills) {
         (void)hipFree(x.q);
         (void)hipFree(x.ws);
+        if (x.rq) (void)hipFree(x.rq);
     }
     delete ctx;
     return 0;

@@ -286,6 +286,37 @@ static void emu_do_reset(const tmg::Params &P, int64_t n, int8_t *board, uint64_
     }
 }
 
+template <int M, int B, bool O>
+struct RqTag {
+    static constexpr int maxn = M, nb = B;
+    static constexpr bool codd = O;
+};
+template <class F>
+static void template_dispatch(const tmg::Params &P, F run) {
+    if (P.N > 128) { run(RqTag<512, 0, false>{}); return; }
+    if (!sb_ok(P)) { run(RqTag<128, 0, false>{}); return; }
+    const bool o = P.C & 1;
+    switch (tmg::sb_planes(P.k)) {
+    case 1: if (o) run(RqTag<128, 1, true>{}); else run(RqTag<128, 1, false>{}); break;
+    case 2: if (o) run(RqTag<128, 2, true>{}); else run(RqTag<128, 2, false>{}); break;
+    case 3: if (o) run(RqTag<128, 3, true>{}); else run(RqTag<128, 3, false>{}); break;
+    default: if (o) run(RqTag<128, 4, true>{}); else run(RqTag<128, 4, false>{}); break;
+    }
+}
+
+// the deferred autoresets through the queue, as tmg_capi.hip's do_step
+static std::vector<unsigned char> g_rq;
+static void emu_reset_queued(const tmg::Params &P, int64_t n, int8_t *board, uint64_t *rng, int32_t *timer,
+                             uint64_t *eff) {
+    const int64_t g = n < 64 ? n : 64;
+    auto run = [&](auto tag) {
+        constexpr int MAXN = decltype(tag)::maxn, NB = decltype(tag)::nb;
+        constexpr bool CODD = decltype(tag)::codd;
+        run_grid(g, sizeof(tmg::Ws<MAXN, false>), [&] { tmg::reset_queue_kernel<MAXN, NB, CODD>(P, board, rng, timer, eff); });
+    };
+    template_dispatch(P, run);
+}
+
 extern "C" {
 
 int emu_step(int R, int C, int k, int smask, int moves, int64_t n, int8_t *board, uint64_t *rng, int32_t *timer,
@@ -293,6 +324,8 @@ int emu_step(int R, int C, int k, int smask, int moves, int64_t n, int8_t *board
              int trust_eff, int autoreset) {
     if (!g_jump_init) { tmg::build_jump_table(g_jump); g_jump_init = true; }
     tmg::Params P = make_params(R, C, k, smask, moves, g_jump);
+    g_rq.assign(sizeof(tmg::ResetQ) + (size_t)n * sizeof(int64_t), 0);
+    P.resetq = reinterpret_cast<tmg::ResetQ *>(g_rq.data());
     EmuStep S;
     S.P = &P; S.n = n; S.board = board; S.rng = rng; S.timer = timer; S.actions = actions; S.reward = reward;
     S.n_new = n_new; S.n_act = n_act; S.flags = flags; S.eff = eff; S.trust_eff = trust_eff; S.autoreset = autoreset;
@@ -304,7 +337,7 @@ int emu_step(int R, int C, int k, int smask, int moves, int64_t n, int8_t *board
                 const int deferred = TMG_LEAN_DEFER ? S.autoreset : 0;    // as tmg_capi.hip's do_step
                 if (deferred) S.autoreset = 2;
                 if (P.C & 1) emu_step_sb<false, true>(S); else emu_step_sb<false, false>(S);
-                if (deferred) emu_do_reset(P, n, board, rng, timer, eff, flags, tmg::FL_RESET);
+                if (deferred) emu_reset_queued(P, n, board, rng, timer, eff);
             }
             else {
                 // general kernel: autoreset deferred to a FL_RESET-masked reset, as tmg_capi.hip
@@ -312,13 +345,13 @@ int emu_step(int R, int C, int k, int smask, int moves, int64_t n, int8_t *board
                 if (deferred) S.autoreset = 2;
                 if (P.C & 1) emu_step_sb<true, true>(S); else emu_step_sb<true, false>(S);
                 emu_spill<128>(S);
-                if (deferred) emu_do_reset(P, n, board, rng, timer, eff, flags, tmg::FL_RESET);
+                if (deferred) emu_reset_queued(P, n, board, rng, timer, eff);
             }
         } else if (lean) {
             const int deferred = TMG_LEAN_DEFER ? S.autoreset : 0;
             if (deferred) S.autoreset = 2;
             emu_step_kernel<128, false, 0, false>(S);
-            if (deferred) emu_do_reset(P, n, board, rng, timer, eff, flags, tmg::FL_RESET);
+            if (deferred) emu_reset_queued(P, n, board, rng, timer, eff);
         } else {
             emu_step_kernel<128, true, 0, false>(S);
             emu_spill<128>(S);
@@ -333,7 +366,7 @@ int emu_step(int R, int C, int k, int smask, int moves, int64_t n, int8_t *board
         emu_step_kernel<512, true, 0, false>(S);
         emu_spill<512>(S);
     }
-    if (deferred) emu_do_reset(P, n, board, rng, timer, eff, flags, tmg::FL_RESET);
+    if (deferred) emu_reset_queued(P, n, board, rng, timer, eff);
     return 0;
 }
 
