@@ -172,6 +172,8 @@ def main():
     ap.add_argument("--phase-blocks", type=int, default=3,
                     help="episode phase blocks: P contiguous env blocks offset by 30/P steps (1 = aligned, "
                          "0 = every env staggered)")
+    ap.add_argument("--phase-interleave", action="store_true",
+                    help="env i in phase block i mod P (every env group holds all blocks) instead of contiguous blocks")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--dry-run", action="store_true", help="print each rank's shard layout and exit (no GPU)")
     args = ap.parse_args()
@@ -209,7 +211,7 @@ def main():
     acts = torch.from_numpy(synthetic_actions(rng_, T, A)).to(dev)
     env.reset()
     if args.phase_blocks != 1:
-        env.stagger_phases(blocks=args.phase_blocks, first_env=rng_.start)
+        env.stagger_phases(blocks=args.phase_blocks, first_env=rng_.start, interleave=args.phase_interleave)
     env.status(clear=True)
 
     def step(t):

@@ -11,8 +11,8 @@ for lib in ${LIBS:-libtmg.so}; do
     echo "== $lib"; grep groups gpurun_out/lat_$lib.log
   fi
   for spec in ${SPECS:-3:20:5 3:300:30 1:300:30 0:60:30}; do
-    IFS=: read -r p1 p2 p3 <<< "$spec"; set -- $p1 $p2 $p3
-    timeout -k 10 300 python bench.py --phase-blocks $1 --steps $2 --warmup $3 --no-cpu-baseline > gpurun_out/bench_${lib}_p$1_k$2.log 2>&1 || { tail -3 gpurun_out/bench_${lib}_p$1_k$2.log; exit 1; }
-    tail -1 gpurun_out/bench_${lib}_p$1_k$2.log | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print('BENCH $lib P=$1 K=$2', d['value'], 'ms/step', d['ms_per_step'])"
+    IFS=: read -r p1 p2 p3 p4 <<< "$spec"; set -- $p1 $p2 $p3 $p4
+    timeout -k 10 300 python bench.py --phase-blocks $1 --steps $2 --warmup $3 ${4:+--phase-interleave} --no-cpu-baseline > gpurun_out/bench_${lib}_p$1_k$2.log 2>&1 || { tail -3 gpurun_out/bench_${lib}_p$1_k$2.log; exit 1; }
+    tail -1 gpurun_out/bench_${lib}_p$1_k$2.log | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print('BENCH $lib P=$1 K=$2 I=$4', d['value'], 'ms/step', d['ms_per_step'])"
   done
 done

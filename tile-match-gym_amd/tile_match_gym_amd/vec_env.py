@@ -115,7 +115,7 @@ class TileMatchVecEnv:
         w = batch_rng_words(seeds)
         self.rng.copy_(torch.from_numpy(w.view(np.int64)))
 
-    def stagger_phases(self, blocks: int = 0, first_env: int = 0):
+    def stagger_phases(self, blocks: int = 0, first_env: int = 0, interleave: bool = False):
         """Offset the episode phases right after a reset by setting timers.  A
         timer of m is the state after m ineffective moves (board.py:352-353: no
         board or RNG change; tile_match_env.py:100 counts the move).
@@ -128,11 +128,18 @@ class TileMatchVecEnv:
         j * M / Pg + g * M / (Pg * groups) (M = num_moves, floors).  Every
         group then finishes a sub-block's episodes every M / Pg steps, and the
         groups take turns, so a window of a multiple of M / Pg steps holds the
-        same reset work on every group's stream."""
+        same reset work on every group's stream.
+        interleave=True: env i belongs to block i mod P instead, so every group
+        stream holds an equal part of every block's resets."""
         self.join()
         N, M = self.num_envs, self.num_moves
         if blocks == 1:
             self.timer.zero_()
+        elif blocks and blocks > 0 and interleave:
+            # interleaved blocks: env i in block i mod P (every env group holds
+            # all P blocks), block b starting at b * M // P
+            i = torch.arange(N, device=self.device, dtype=torch.int64)
+            self.timer.copy_(((i % blocks) * M // blocks % M).to(torch.int32))
         elif blocks and blocks > 0:
             G = len(self._ranges)
             Pg = max(1, -(-int(blocks) // G))
