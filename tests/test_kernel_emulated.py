@@ -61,6 +61,9 @@ def test_trajectory_golden_emulated(emu_lib, name, autoreset, monkeypatch):
     (11, 11, 4, 0), (10, 10, 4, 14), (8, 8, 3, 15), (5, 12, 6, 15),
     # 512-cell kernels: rows straddle the 64-cell passes unevenly (bounded line search)
     (16, 24, 7, 0), (24, 21, 7, 9),
+    # 512-cell general kernels with specials: wave-parallel simple / laser steps
+    # (simple_step_lds) beside the lane-0 list machinery
+    (20, 20, 6, 15), (12, 12, 5, 15), (16, 16, 6, 6),
 ])
 def test_random_rollouts_emulated(emu_lib, cfg):
     """Random-action rollouts with autoreset: emulated kernels vs the oracle, every field, every step."""

@@ -1014,6 +1014,114 @@ __device__ __forceinline__ int fast_clear(const Params &P, WS &w, int lane, cons
     return cleared;
 }
 
+// Whether every cell is a coloured tile of type >= 1 with colour 1..k or a
+// colourless cookie: then equal colours >= 1 imply types >= 1, so the line
+// runs of get_colour_lines (which extend by colour only, board.py:163-193) are
+// exactly the anchored runs of detect().  Empties and cookies that gained a
+// colour (remove_colour_lines after a shuffle, :129) fail it.  A cascade keeps
+// it: refill draws type-1 tiles, create_special gives a cookie colour 0.
+template <class WS>
+__device__ __forceinline__ bool plain_board(const Params &P, const WS &w, int lane) {
+    const int N = P.N;
+    bool odd = false;
+    for (int p = lane; p < N; p += 64) {
+        const int x = w.brd[p], y = w.brd[N + p];
+        odd |= y == 0 || (y < 0 && x != 0) || (y > 0 && (x < 1 || x > P.k));
+    }
+    return __ballot(odd) == 0ULL;
+}
+
+// One cascade step of the general kernel (board.py:367-376) on the LDS board,
+// wave-parallel, when it needs none of the lane-0 list machinery — the form of
+// sb_simple_step for boards without a bitboard path (the 512-cell kernels).
+// Requires plain_board().  The step qualifies when get_colour_lines (:149-215)
+// yields no perpendicular line, process_colour_lines (:269-327) makes every
+// first-pass line of row rs a normal match or a laser (no 5+-line when cookies
+// are enabled; no two lines sharing a cell when bombs are or a laser is
+// created) and no line cell holds a special (resolve_colour_match :460-471).
+// A straight 4-line's laser goes to its second cell in (row, col) order
+// (get_special_creation_pos :429-458, nothing taken): (rs, s+1) / (top+1, c).
+// Returns 0 when the step does not qualify (LDS board and marks untouched),
+// otherwise the number of cleared cells (cleared in LDS, lasers placed,
+// SC_NNEW counted); gravity and refill are the caller's.
+template <class WS>
+__device__ __forceinline__ int simple_step_lds(const Params &P, WS &w, int lane, const Det<WS::NP> &d, int rs) {
+    const int C = P.C, R = P.R, N = P.N, S = P.smask;
+    int8_t *col = w.brd, *typ = w.brd + N;
+    const uint64_t cm = C >= 64 ? ~0ULL : (1ULL << C) - 1;
+    // horizontal runs of row rs: an L-run holds L-2 consecutive anchor bits
+    const uint64_t hb = bits_at(d.h, rs * C, C), vb = bits_at(d.v, rs * C, C);
+    const uint64_t st = hb & ~(hb << 1);
+    const uint64_t h4 = st & (hb >> 1) & ~(hb >> 2), h5 = st & (hb >> 1) & (hb >> 2);
+    if (h5 && (S & SP_COOKIE)) return 0;
+    const uint64_t cov = (hb | (hb << 1) | (hb << 2)) & cm;
+    const uint64_t hl = (S & (SP_HLASER | SP_VLASER)) ? h4 << 1 : 0ULL;   // laser cells (columns of row rs)
+    // vertical runs ending in row rs: lane c keeps the top row of column c's run
+    int vt = R;
+    uint64_t vl = 0;                                                         // columns of vertical 4-lines
+    for (uint64_t m = vb; m; m &= m - 1) {
+        const int c = __ffsll((unsigned long long)m) - 1;
+        const int top = run_top(P, w, lane, rs, c);
+        const int L = rs - top + 1;
+        if (L >= 5 && (S & SP_COOKIE)) return 0;
+        if (L == 4 && (S & SP_VLASER)) vl |= 1ULL << c;
+        vt = lane == c ? top : vt;
+    }
+    if ((vb & cov) && ((S & SP_BOMB) || hl || vl)) return 0;
+    // coords K: lane-parallel over the cells, K = row rs's runs + the column runs
+    const int th = (S & SP_HLASER) ? 3 : 2;
+    bool bad = false;
+    for (int p0 = 0; p0 < N; p0 += 64) {                                    // uniform passes (bpermute)
+        const int p = p0 + lane;
+        const int r = div_c(P, p), c = p - r * C;
+        const int top = __builtin_amdgcn_ds_bpermute((c & 63) << 2, vt);
+        const bool k = p < N && ((r == rs && ((cov >> c) & 1)) || (((vb >> c) & 1) && r >= top && r <= rs));
+        bad |= k && typ[p] != 1;
+        if (k) w.mark[p] = 1;
+    }
+    WSYNC();
+    // get_colour_lines' perpendicular pass (:195-214): from every coord walk each
+    // axis over non-coord cells of the same colour; a run of >= 3 is a line
+    for (int p = lane; p < N; p += 64) {
+        if (!w.mark[p]) continue;
+        const int r = div_c(P, p), c = p - r * C, x = col[p];
+        int lft = 0, rgt = 0, up = 0, dn = 0;
+        while (c - lft - 1 >= 0 && !w.mark[p - lft - 1] && col[p - lft - 1] == x) lft++;
+        while (c + rgt + 1 < C && !w.mark[p + rgt + 1] && col[p + rgt + 1] == x) rgt++;
+        while (r - up - 1 >= 0 && !w.mark[p - (up + 1) * C] && col[p - (up + 1) * C] == x) up++;
+        while (r + dn + 1 < R && !w.mark[p + (dn + 1) * C] && col[p + (dn + 1) * C] == x) dn++;
+        bad |= lft + rgt >= 2 || up + dn >= 2;
+    }
+    const bool ok = __ballot(bad) == 0ULL;
+    WSYNC();
+    // resolve: clear the coords (no special among them), then place the lasers
+    int cleared = 0;
+    for (int p0 = 0; p0 < N; p0 += 64) {
+        const int p = p0 + lane;
+        const bool k = p < N && w.mark[p];
+        const int r = div_c(P, p), c = p - r * C;
+        const int top = __builtin_amdgcn_ds_bpermute((c & 63) << 2, vt);
+        bool pos = false;
+        int t = 2;
+        if (k) {
+            const bool ph = r == rs && ((hl >> c) & 1);
+            const bool pv = ((vl >> c) & 1) && r == top + 1;
+            pos = ph || pv;
+            t = ph ? th : 2;
+            w.mark[p] = 0;
+            if (ok) {
+                if (pos) typ[p] = (int8_t)t;
+                else { col[p] = 0; typ[p] = 0; }
+            }
+        }
+        cleared += __popcll(__ballot(k && !pos));
+    }
+    if (!ok) { WSYNC(); return 0; }
+    if (lane == 0) w.sc[SC_NNEW] += __popcll(hl) + __popcll(vl);
+    WSYNC();
+    return cleared;
+}
+
 // ------------------------------------------------------------ general (lane 0)
 // Everything below runs on lane 0 only, against LDS.
 template <int MAXN, class LS = WsSerial<MAXN>>
@@ -1469,6 +1577,10 @@ __device__ __forceinline__ int board_move(const Params &P, Ws<MAXN, GEN> &w, int
         for (int p = lane; p < N; p += 64) ok &= typ[p] == 1;
         fast = __ballot(!ok) == 0ULL;
     }
+    // 512-cell general kernels (no bitboard path): wave-parallel steps while
+    // the board stays plain (plain_board is kept by every cascade step)
+    bool plain = false;
+    if constexpr (GEN && SBNB == 0) plain = !fast && !ovf && !err && plain_board(P, w, lane);
     int iters = 0;
     (void)e;
     while (!ovf && !err) {                                                  // :367-376
@@ -1486,6 +1598,17 @@ __device__ __forceinline__ int board_move(const Params &P, Ws<MAXN, GEN> &w, int
         if (fast) {
             elim += fast_clear(P, w, lane, cl, d, rs);
         } else {
+            if constexpr (GEN && SBNB == 0) {
+                const int r = plain ? simple_step_lds(P, w, lane, d, rs) : 0;
+                if (r > 0) {
+                    elim += r;
+                    gravity(P, w, lane);
+                    WSYNC();
+                    refill(P, w, lane, J, g);
+                    iters++;
+                    continue;
+                }
+            }
             if constexpr (GEN) {
                 int nz = count_colour_nonzero(P, w, lane);
                 if (lane == 0) {

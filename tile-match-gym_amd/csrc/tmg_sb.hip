@@ -530,11 +530,10 @@ __device__ __forceinline__ int sb_move(const Params &P, WS &w, int lane, const L
 // One cascade step of the general kernel (specials enabled, board.py:367-376)
 // on bitboards, when it provably reduces to the no-specials union clear:
 // get_colour_lines yields no perpendicular line, process_colour_lines
-// (:269-327) turns every first-pass line into a normal match — no 4-line when
-// a laser is enabled (a horizontal one only counts for the h-laser or the
-// v-laser, a vertical one for the v-laser, :294-302), no 5+-line when cookies
-// are, no two lines sharing a cell when bombs are (:304-320) — and no cleared
-// cell holds a special to activate (resolve_colour_match, :460-471).
+// (:269-327) turns every first-pass line into a normal match or a laser — no
+// 5+-line when cookies are enabled, no two lines sharing a cell when bombs are
+// (:304-320) or a laser is created — and no cleared cell holds a special to
+// activate (resolve_colour_match, :460-471).
 // Returns -1 when there is no line, 0 when the step is not of that kind (the
 // caller runs the list machinery on the unchanged LDS board), otherwise the
 // number of cleared cells (the board in LDS has been cleared, dropped and
@@ -566,17 +565,35 @@ __device__ __forceinline__ int sb_simple_step(const Params &P, WS &w, int lane, 
     const bool h5 = nonzero(h2 & bwd<false>(h, 2));
     const Pair x4 = bwd<CODD>(bwd<false>(d.va & row, 2 * C) & eqU, C);    // 4th cell of a vertical run
     const bool v4 = nonzero(andn(x4, eqU)), v5 = nonzero(x4 & eqU);
-    if (h4 && (S & (SP_HLASER | SP_VLASER))) return 0;
-    if (v4 && (S & SP_VLASER)) return 0;
     if ((h5 || v5) && (S & SP_COOKIE)) return 0;
+    // 4-lines become lasers (:294-302): a horizontal one an h-laser (a v-laser
+    // when only that is enabled), a vertical one a v-laser.  With no line sharing
+    // a cell, nothing is taken (:429-458) and a straight 4-line's creation cell
+    // is its second cell in (row, col) order: (rs, s+1) for a horizontal run
+    // starting at s, (top+1, c) for a vertical one.
+    const bool hl = h4 && (S & (SP_HLASER | SP_VLASER)), vl = v4 && (S & SP_VLASER);
     Pair kh, kv;
     sb_coords<CODD>(P, d, rs, kh, kv);
-    if ((S & SP_BOMB) && nonzero(kh & kv)) return 0;
+    if (((S & SP_BOMB) || hl || vl) && nonzero(kh & kv)) return 0;
     const Pair K = kh | kv;
     const Pair sp{__ballot(y0 >= 2), __ballot(y1 >= 2)};                  // lasers / bombs
     if (nonzero(K & sp)) return 0;
     Pair clr = K;
     if (sb_perpendicular<CODD>(P, d, K, clr)) return 0;
+    if (hl || vl) {
+        const Pair ph = hl ? fwd<true>(andn(andn(h2, bwd<false>(h, 2)), fwd<true>(h, 1)), 1) : Pair{0, 0};
+        const Pair pv = vl ? fwd<CODD>(andn(x4, eqU), C) : Pair{0, 0};
+        const int th = (S & SP_HLASER) ? 3 : 2;                            // create_special :572-597
+        int8_t *ty = w.brd + N;
+        // the lane owning the cell writes its type; sb_gravity_refill reads it back on the same lane
+        *(test(ph, q0) ? ty + q0 : w.trash + lane) = (int8_t)th;
+        *(test(ph, q0 + 1) ? ty + q0 + 1 : w.trash + 64 + lane) = (int8_t)th;
+        *(test(pv, q0) ? ty + q0 : w.trash + 128 + lane) = (int8_t)2;
+        *(test(pv, q0 + 1) ? ty + q0 + 1 : w.trash + 192 + lane) = (int8_t)2;
+        const Pair pos = ph | pv;
+        clr = andn(clr, pos);
+        if (lane == 0) w.sc[SC_NNEW] += popc(pos);
+    }
     const int tot = popc(clr);
     sb_gravity_refill<CODD, true>(P, w, lane, J, g, clr, tot, c);
     return tot;
