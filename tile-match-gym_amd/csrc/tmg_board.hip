@@ -1014,6 +1014,38 @@ __device__ __forceinline__ int fast_clear(const Params &P, WS &w, int lane, cons
     return cleared;
 }
 
+// process_colour_lines' bomb rule (board.py:304-320) for the first-pass lines
+// of one row rs, as column masks of that row: hb = horizontal anchor columns
+// (a run of L cells holds L-2 consecutive bits), x = the columns where a
+// vertical line ending in row rs meets a horizontal run (the shared cell).
+// The verticals sort first (their first coord lies above row rs), so each such
+// vertical makes a bomb with the run it meets: its cells + the two run cells
+// nearest the shared one (by distance, then column, :309-312), and a run of
+// < 6 cells then leaves the list with its other cells uncleared (:314-315).
+// The bomb goes to the shared cell: get_special_creation_pos' corner
+// (:437-447), the bomb's most common row (rs) and column (the vertical's).
+// Handled when every vertical is 3 or >= 5 long (the caller's check), each run
+// meets one vertical and is at most 5 long; false otherwise.  keep: the run
+// cells that stay on the board.
+__device__ __forceinline__ bool bomb_plan(uint64_t hb, uint64_t x, uint64_t &keep) {
+    const uint64_t st = hb & ~(hb << 1);                                     // run starts
+    keep = 0;
+    for (uint64_t m = x; m; m &= m - 1) {
+        const int c = __ffsll((unsigned long long)m) - 1;
+        const uint64_t le = st & (c >= 63 ? ~0ULL : (2ULL << c) - 1);        // starts <= c
+        if (!le) return false;
+        const int s = 63 - __clzll(le);
+        const int len = __ffsll((unsigned long long)~(hb >> s)) + 1;         // anchors + 2
+        if (len > 5) return false;
+        const uint64_t run = ((1ULL << len) - 1) << s;
+        if (__popcll(x & run) != 1) return false;
+        const int e = s + len - 1;
+        const uint64_t take = (1ULL << c) | (c > s && c < e ? (5ULL << (c - 1)) : c == s ? (3ULL << (c + 1)) : (3ULL << (c - 2)));
+        keep |= run & ~take;
+    }
+    return true;
+}
+
 // Whether every cell is a coloured tile of type >= 1 with colour 1..k or a
 // colourless cookie: then equal colours >= 1 imply types >= 1, so the line
 // runs of get_colour_lines (which extend by colour only, board.py:163-193) are
@@ -1036,9 +1068,9 @@ __device__ __forceinline__ bool plain_board(const Params &P, const WS &w, int la
 // sb_simple_step for boards without a bitboard path (the 512-cell kernels).
 // Requires plain_board().  The step qualifies when get_colour_lines (:149-215)
 // yields no perpendicular line, process_colour_lines (:269-327) makes every
-// first-pass line of row rs a normal match or a laser (no 5+-line when cookies
-// are enabled; no two lines sharing a cell when bombs are or a laser is
-// created) and no line cell holds a special (resolve_colour_match :460-471).
+// first-pass line of row rs a normal match, a laser or a bomb of bomb_plan (no
+// 5+-line when cookies are enabled; no two lines sharing a cell when a laser
+// is created) and no line cell holds a special (resolve_colour_match :460-471).
 // A straight 4-line's laser goes to its second cell in (row, col) order
 // (get_special_creation_pos :429-458, nothing taken): (rs, s+1) / (top+1, c).
 // Returns 0 when the step does not qualify (LDS board and marks untouched),
@@ -1059,15 +1091,22 @@ __device__ __forceinline__ int simple_step_lds(const Params &P, WS &w, int lane,
     // vertical runs ending in row rs: lane c keeps the top row of column c's run
     int vt = R;
     uint64_t vl = 0;                                                         // columns of vertical 4-lines
+    bool v4 = false;
     for (uint64_t m = vb; m; m &= m - 1) {
         const int c = __ffsll((unsigned long long)m) - 1;
         const int top = run_top(P, w, lane, rs, c);
         const int L = rs - top + 1;
         if (L >= 5 && (S & SP_COOKIE)) return 0;
+        v4 |= L == 4;
         if (L == 4 && (S & SP_VLASER)) vl |= 1ULL << c;
         vt = lane == c ? top : vt;
     }
-    if ((vb & cov) && ((S & SP_BOMB) || hl || vl)) return 0;
+    // shared cells: lines sharing a cell are separate normal matches without
+    // bombs; with bombs they follow bomb_plan
+    const uint64_t x = vb & cov, bombc = (S & SP_BOMB) ? x : 0ULL;
+    uint64_t keepc = 0;
+    if (x && (hl || vl)) return 0;
+    if (bombc && (h4 || v4 || !bomb_plan(hb, bombc, keepc))) return 0;
     // coords K: lane-parallel over the cells, K = row rs's runs + the column runs
     const int th = (S & SP_HLASER) ? 3 : 2;
     bool bad = false;
@@ -1101,23 +1140,25 @@ __device__ __forceinline__ int simple_step_lds(const Params &P, WS &w, int lane,
         const bool k = p < N && w.mark[p];
         const int r = div_c(P, p), c = p - r * C;
         const int top = __builtin_amdgcn_ds_bpermute((c & 63) << 2, vt);
-        bool pos = false;
+        bool pos = false, keep = false;
         int t = 2;
         if (k) {
             const bool ph = r == rs && ((hl >> c) & 1);
             const bool pv = ((vl >> c) & 1) && r == top + 1;
-            pos = ph || pv;
-            t = ph ? th : 2;
+            const bool pb = r == rs && ((bombc >> c) & 1);
+            keep = r == rs && ((keepc >> c) & 1);
+            pos = ph || pv || pb;
+            t = ph ? th : pb ? 4 : 2;
             w.mark[p] = 0;
             if (ok) {
                 if (pos) typ[p] = (int8_t)t;
-                else { col[p] = 0; typ[p] = 0; }
+                else if (!keep) { col[p] = 0; typ[p] = 0; }
             }
         }
-        cleared += __popcll(__ballot(k && !pos));
+        cleared += __popcll(__ballot(k && !pos && !keep));
     }
     if (!ok) { WSYNC(); return 0; }
-    if (lane == 0) w.sc[SC_NNEW] += __popcll(hl) + __popcll(vl);
+    if (lane == 0) w.sc[SC_NNEW] += __popcll(hl) + __popcll(vl) + __popcll(bombc);
     WSYNC();
     return cleared;
 }

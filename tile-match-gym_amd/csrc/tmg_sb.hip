@@ -530,10 +530,10 @@ __device__ __forceinline__ int sb_move(const Params &P, WS &w, int lane, const L
 // One cascade step of the general kernel (specials enabled, board.py:367-376)
 // on bitboards, when it provably reduces to the no-specials union clear:
 // get_colour_lines yields no perpendicular line, process_colour_lines
-// (:269-327) turns every first-pass line into a normal match or a laser — no
-// 5+-line when cookies are enabled, no two lines sharing a cell when bombs are
-// (:304-320) or a laser is created — and no cleared cell holds a special to
-// activate (resolve_colour_match, :460-471).
+// (:269-327) turns every first-pass line into a normal match, a laser or a
+// bomb of bomb_plan — no 5+-line when cookies are enabled, no two lines
+// sharing a cell when a laser is created — and no cleared cell holds a
+// special to activate (resolve_colour_match, :460-471).
 // Returns -1 when there is no line, 0 when the step is not of that kind (the
 // caller runs the list machinery on the unchanged LDS board), otherwise the
 // number of cleared cells (the board in LDS has been cleared, dropped and
@@ -574,7 +574,18 @@ __device__ __forceinline__ int sb_simple_step(const Params &P, WS &w, int lane, 
     const bool hl = h4 && (S & (SP_HLASER | SP_VLASER)), vl = v4 && (S & SP_VLASER);
     Pair kh, kv;
     sb_coords<CODD>(P, d, rs, kh, kv);
-    if (((S & SP_BOMB) || hl || vl) && nonzero(kh & kv)) return 0;
+    // lines sharing a cell: separate normal matches without bombs, bomb_plan with
+    uint64_t bombc = 0, keepc = 0;
+    if (nonzero(kh & kv)) {
+        if (hl || vl) return 0;
+        if (S & SP_BOMB) {
+            if (h4 || v4) return 0;
+            const int q = rs * C + lane;                                   // row rs as column masks
+            const uint64_t hbc = __ballot(lane < C && test(h, q));
+            bombc = __ballot(lane < C && test(kh & kv, q));
+            if (!bomb_plan(hbc, bombc, keepc)) return 0;
+        }
+    }
     const Pair K = kh | kv;
     const Pair sp{__ballot(y0 >= 2), __ballot(y1 >= 2)};                  // lasers / bombs
     if (nonzero(K & sp)) return 0;
@@ -593,6 +604,17 @@ __device__ __forceinline__ int sb_simple_step(const Params &P, WS &w, int lane, 
         const Pair pos = ph | pv;
         clr = andn(clr, pos);
         if (lane == 0) w.sc[SC_NNEW] += popc(pos);
+    }
+    if (bombc) {
+        const int r0 = div_c(P, q0), r1 = div_c(P, q0 + 1);
+        const int c0 = q0 - rs * C, c1 = q0 + 1 - rs * C;
+        const bool b0 = r0 == rs && ((bombc >> c0) & 1), b1 = r1 == rs && ((bombc >> c1) & 1);
+        const bool k0 = r0 == rs && ((keepc >> c0) & 1), k1 = r1 == rs && ((keepc >> c1) & 1);
+        int8_t *ty = w.brd + N;
+        *(b0 ? ty + q0 : w.trash + lane) = (int8_t)4;
+        *(b1 ? ty + q0 + 1 : w.trash + 64 + lane) = (int8_t)4;
+        clr = andn(clr, Pair{__ballot(b0 || k0), __ballot(b1 || k1)});
+        if (lane == 0) w.sc[SC_NNEW] += __popcll(bombc);
     }
     const int tot = popc(clr);
     sb_gravity_refill<CODD, true>(P, w, lane, J, g, clr, tot, c);
