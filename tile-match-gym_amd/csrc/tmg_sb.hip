@@ -548,7 +548,7 @@ __device__ __forceinline__ int sb_simple_step(const Params &P, WS &w, int lane, 
     // the bitboards model tiles of type >= 1 with colours 1..k and colourless
     // cookies; empty cells (gravity would move them too), cookies that gained a
     // colour (remove_colour_lines, :129) and out-of-range values take the list path
-    const auto odd_cell = [&](int x, int y) { return y == 0 || (y < 0 && x != 0) || x < 0 || x > P.k; };
+    const auto odd_cell = [&](int x, int y) { return y == 0 || y > 4 || y < -1 || (y < 0 && x != 0) || x < 0 || x > P.k; };
     if (__ballot(odd_cell(x0, y0) || odd_cell(x1, y1)) != 0ULL) return 0;
     SBC c{x0 - 1, x1 - 1};
     const Pair z{__ballot(x0 == 0), __ballot(x1 == 0)};                    // colourless (cookies)
@@ -587,34 +587,77 @@ __device__ __forceinline__ int sb_simple_step(const Params &P, WS &w, int lane, 
         }
     }
     const Pair K = kh | kv;
-    const Pair sp{__ballot(y0 >= 2), __ballot(y1 >= 2)};                  // lasers / bombs
-    if (nonzero(K & sp)) return 0;
     Pair clr = K;
     if (sb_perpendicular<CODD>(P, d, K, clr)) return 0;
+    const Pair sp{__ballot(y0 >= 2), __ballot(y1 >= 2)};                  // lasers / bombs
+    // specials on matched cells activate (resolve_colour_match :460-471).  With
+    // no cookie on the board (the only order-dependent special) the result is
+    // the closure: each activated special clears its column (v-laser), row
+    // (h-laser) or 3x3 (bomb) and activates the specials there (:473-525).
+    const bool act = nonzero(K & sp);
+    if (act && nonzero(z)) return 0;
+    // creation cells (create_special :572-597, after every activation) and the
+    // bomb runs' cells that stay
+    Pair pos{0, 0}, keep{0, 0};
+    int8_t *ty = w.brd + N;
     if (hl || vl) {
         const Pair ph = hl ? fwd<true>(andn(andn(h2, bwd<false>(h, 2)), fwd<true>(h, 1)), 1) : Pair{0, 0};
         const Pair pv = vl ? fwd<CODD>(andn(x4, eqU), C) : Pair{0, 0};
-        const int th = (S & SP_HLASER) ? 3 : 2;                            // create_special :572-597
-        int8_t *ty = w.brd + N;
+        const int th = (S & SP_HLASER) ? 3 : 2;
         // the lane owning the cell writes its type; sb_gravity_refill reads it back on the same lane
         *(test(ph, q0) ? ty + q0 : w.trash + lane) = (int8_t)th;
         *(test(ph, q0 + 1) ? ty + q0 + 1 : w.trash + 64 + lane) = (int8_t)th;
         *(test(pv, q0) ? ty + q0 : w.trash + 128 + lane) = (int8_t)2;
         *(test(pv, q0 + 1) ? ty + q0 + 1 : w.trash + 192 + lane) = (int8_t)2;
-        const Pair pos = ph | pv;
-        clr = andn(clr, pos);
-        if (lane == 0) w.sc[SC_NNEW] += popc(pos);
+        pos = ph | pv;
     }
     if (bombc) {
         const int r0 = div_c(P, q0), r1 = div_c(P, q0 + 1);
         const int c0 = q0 - rs * C, c1 = q0 + 1 - rs * C;
         const bool b0 = r0 == rs && ((bombc >> c0) & 1), b1 = r1 == rs && ((bombc >> c1) & 1);
         const bool k0 = r0 == rs && ((keepc >> c0) & 1), k1 = r1 == rs && ((keepc >> c1) & 1);
-        int8_t *ty = w.brd + N;
         *(b0 ? ty + q0 : w.trash + lane) = (int8_t)4;
         *(b1 ? ty + q0 + 1 : w.trash + 64 + lane) = (int8_t)4;
-        clr = andn(clr, Pair{__ballot(b0 || k0), __ballot(b1 || k1)});
-        if (lane == 0) w.sc[SC_NNEW] += __popcll(bombc);
+        pos = pos | Pair{__ballot(b0), __ballot(b1)};
+        keep = Pair{__ballot(k0), __ballot(k1)};
+    }
+    clr = andn(K, keep);                                                   // matched cells
+    if (act) {
+        const Pair vls{__ballot(y0 == 2), __ballot(y1 == 2)}, hls{__ballot(y0 == 3), __ballot(y1 == 3)};
+        const Pair inb{P.sb_in[0], P.sb_in[1]};
+        Pair done{0, 0}, front = clr & sp;
+        while (nonzero(front)) {
+            const int s = front.a ? 2 * ctz64(front.a) : 2 * ctz64(front.b) + 1;
+            const Pair bit{(s & 1) ? 0ULL : 1ULL << (s >> 1), (s & 1) ? 1ULL << (s >> 1) : 0ULL};
+            done = done | bit;
+            const int r = div_c(P, s), cc = s - r * C;
+            Pair area;
+            if (nonzero(bit & vls)) {                                      // v-laser: column cc
+                if constexpr (CODD) {
+                    area = Pair{P.sb_z << ((((cc & 1) * C) + cc) >> 1), P.sb_z << ((((1 - (cc & 1)) * C) + cc) >> 1)};
+                } else {
+                    area = (cc & 1) ? Pair{0, P.sb_z << (cc >> 1)} : Pair{P.sb_z << (cc >> 1), 0};
+                }
+                area = area & inb;
+            } else if (nonzero(bit & hls)) {                               // h-laser: row r
+                area = sb_row(P, r);
+            } else {                                                       // bomb: 3x3
+                area = Pair{0, 0};
+                for (int i = r > 0 ? r - 1 : 0; i <= (r + 1 < P.R ? r + 1 : P.R - 1); i++)
+                    for (int j = cc > 0 ? cc - 1 : 0; j <= (cc + 1 < C ? cc + 1 : C - 1); j++) {
+                        const int q = i * C + j;
+                        if (q & 1) area.b |= 1ULL << (q >> 1);
+                        else area.a |= 1ULL << (q >> 1);
+                    }
+            }
+            clr = clr | area;
+            front = andn(clr & sp, done);
+        }
+        if (lane == 0) w.sc[SC_NACT] += popc(done);
+    }
+    if (nonzero(pos)) {
+        clr = andn(clr, pos);
+        if (lane == 0) w.sc[SC_NNEW] += popc(pos);
     }
     const int tot = popc(clr);
     sb_gravity_refill<CODD, true>(P, w, lane, J, g, clr, tot, c);
