@@ -54,7 +54,13 @@ namespace tmg {
 #define TMG_STATUS 1           // 0: no sticky status word (A/B of its cost only; tmg_status then reads 0)
 #endif
 #ifndef TMG_GEN128_WAVES
-#define TMG_GEN128_WAVES 4     // min waves per SIMD for the 128-cell general step kernel (caps it at 128 VGPRs)
+#define TMG_GEN128_WAVES 5     // min waves per SIMD for the 128-cell general step kernel (caps it at 96 VGPRs)
+#endif
+#ifndef TMG_RESET_ROLL
+#define TMG_RESET_ROLL 0       // 1: the 512-cell reset kernel's line search as a rolled loop (fewer VGPRs)
+#endif
+#ifndef TMG_LEAN128_WAVES
+#define TMG_LEAN128_WAVES TMG_WPE   // min waves per SIMD for the <= 128-cell lean step kernels (c2)
 #endif
 #ifndef TMG_RQ128_WAVES
 #define TMG_RQ128_WAVES 5      // min waves per SIMD for the 128-cell reset-queue kernel (87 VGPRs, no spill)
@@ -277,7 +283,10 @@ struct ListStore {
 // the general 20x20 kernel fits twice the waves per CU in LDS.  A step that
 // runs out (FL_OVF from the list machinery) is not written back: the env goes
 // to the spill queue and spill_kernel re-runs the step on WsSerialBig.
-template <int MAXN, int CAP = (MAXN > 128 ? MAXN / 2 : MAXN)>
+#ifndef TMG_CAP128
+#define TMG_CAP128 64         // lane-0 list capacity of the <= 128-cell general kernels (cells; more spills)
+#endif
+template <int MAXN, int CAP = (MAXN > 128 ? MAXN / 2 : TMG_CAP128)>
 using WsSerial = ListStore<4 * CAP + 256, CAP + 64, 2 * CAP + 64, CAP + 32, 4 * CAP + 256, CAP + 8>;
 
 // Global-memory lists sized at the worst case of any board of <= MAXN cells
@@ -873,15 +882,17 @@ __device__ __forceinline__ void shuffle(const Params &P, WS &w, int lane, Rng &g
 // (board.py:102-109, 381-391, remove_colour_lines :120-131).  Leaves the final
 // board's effective mask in w.effw.  Returns FL_SHUF when a shuffle ran, FL_ERR
 // when the shuffle cap ended the loop.
+// noline: the board is known to hold no line (the cascade loop just found
+// none), so the first line search is skipped.
 template <bool ROLL = true, class WS>
 __device__ __forceinline__ int ensure_playable(const Params &P, WS &w, int lane, const LaneJump &J, Rng &g,
-                                const Cells<WS::NP> &cl) {
+                                const Cells<WS::NP> &cl, bool noline = false) {
     int fl = 0;
     for (int shuffles = 0;; shuffles++) {
         // Redrawing rows 0..row leaves every cell an anchor test reads in rows
         // > row + 2 unchanged, so after it no anchor lies below max(row + 2, ra).
         int lim = P.R - 1;
-        for (;;) {
+        for (; !noline;) {
             int ra = 0;
             int r0 = first_line_row<ROLL>(P, w, lane, cl, lim, ra);
             if (r0 < 0) break;
@@ -895,6 +906,7 @@ __device__ __forceinline__ int ensure_playable(const Params &P, WS &w, int lane,
         WSYNC();
         shuffle(P, w, lane, g);
         fl = FL_SHUF;
+        noline = false;
     }
     WSYNC();
     return fl;
@@ -1678,7 +1690,8 @@ __device__ __forceinline__ int board_move(const Params &P, Ws<MAXN, GEN> &w, int
     elim += nn;                                                             // :378
     if (ovf) flags |= FL_OVF;
     if (err || w.sc[SC_ERR]) flags |= FL_ERR;
-    flags |= ensure_playable(P, w, lane, J, g, cl);                         // :381-391
+    // the cascade loop ends only on a line-free board (or an error / overflow)
+    flags |= ensure_playable(P, w, lane, J, g, cl, !ovf && !err && !w.sc[SC_ERR]);   // :381-391
     STAMP(e, 3);
     return elim;
 }
@@ -1828,7 +1841,7 @@ __device__ __forceinline__ uint32_t step_env(
 
 // TileMatchEnv.step over a batch, one wave per env.
 template <int MAXN, bool GEN, int SBNB = 0, bool CODD = false>
-__global__ __launch_bounds__(64 * TMG_WPB, (MAXN == 128 && GEN) ? TMG_GEN128_WAVES : TMG_WPE) void step_kernel(
+__global__ __launch_bounds__(64 * TMG_WPB, MAXN == 128 ? (GEN ? TMG_GEN128_WAVES : TMG_LEAN128_WAVES) : TMG_WPE) void step_kernel(
     Params P, int64_t n, int8_t *__restrict__ board, uint64_t *__restrict__ rng, int32_t *__restrict__ timer,
     const int32_t *__restrict__ actions, int32_t *__restrict__ reward, int32_t *__restrict__ n_new,
     int32_t *__restrict__ n_act, uint8_t *__restrict__ flags_out, uint64_t *__restrict__ eff, int trust_eff,
@@ -1894,7 +1907,7 @@ __device__ __forceinline__ void reset_env(const Params &P, WS &w, int lane, int6
     const Cells<MAXN / 64> cl = make_cells<MAXN / 64>(P, lane);
     int fl;
     if constexpr (SBNB > 0) fl = sb_generate<SBNB, CODD, TMG_SB_VDET != 0>(P, w, lane, J, g, cl);   // board.py:95-109
-    else fl = generate_board<false>(P, w, lane, J, g, cl);
+    else fl = generate_board<TMG_RESET_ROLL != 0>(P, w, lane, J, g, cl);
     note_status(P, lane, fl ? ST_INTERNAL : 0u);
     store_board(P, w, lane, board + e * 2 * N);
     store_rng(rng + e * 5, g, lane);
