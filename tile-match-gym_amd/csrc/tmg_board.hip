@@ -59,6 +59,9 @@ namespace tmg {
 #ifndef TMG_RESET_ROLL
 #define TMG_RESET_ROLL 0       // 1: the 512-cell reset kernel's line search as a rolled loop (fewer VGPRs)
 #endif
+#ifndef TMG_RESET_PRE
+#define TMG_RESET_PRE 1        // the 512-cell reset kernel evaluates each redraw's first PCG batch before its line search
+#endif
 #ifndef TMG_LEAN128_WAVES
 #define TMG_LEAN128_WAVES TMG_WPE   // min waves per SIMD for the <= 128-cell lean step kernels (c2)
 #endif
@@ -393,9 +396,14 @@ __device__ __forceinline__ uint32_t r_interval(Rng &g, uint32_t max) {     // ra
 
 // dst[0..M) <- Generator.integers(1, k+1, M) (board.py:97,129,239), lane-parallel:
 // lane j evaluates PCG output j of the batch by jump-ahead; the caller syncs.
+// pre: the batch's first 64 outputs already evaluated (jump-ahead from g), or null
+struct DrawPre {
+    U128 sj;
+    uint64_t out;
+};
 template <class T>
 __device__ __forceinline__ void draw_colours(const Params &P, int lane, const LaneJump &J, Rng &g, int M, T *dst,
-                                             int8_t *trash) {
+                                             int8_t *trash, const DrawPre *pre = nullptr) {
     if (M <= 0) return;
     const uint32_t k = (uint32_t)P.k;
     if (k == 1) {                                          // rng == 0: numpy draws nothing
@@ -416,8 +424,15 @@ __device__ __forceinline__ void draw_colours(const Params &P, int lane, const La
     U128 s{g.slo, g.shi};
     uint64_t last_hi = 0;
     for (int base = 0; base < n64; base += 64) {
-        U128 sj = add128(mul128(J.Aj, s), J.incG);
-        uint64_t out = xsl_rr(sj);
+        U128 sj;
+        uint64_t out;
+        if (pre && base == 0) {
+            sj = pre->sj;
+            out = pre->out;
+        } else {
+            sj = add128(mul128(J.Aj, s), J.incG);
+            out = xsl_rr(sj);
+        }
         const int j = base + lane;
         const uint64_t m0 = (uint64_t)(uint32_t)out * k, m1 = (out >> 32) * k;
         const bool ok0 = j < n64, ok1 = 2 * j + 1 < need;          // ok1 implies ok0
@@ -884,7 +899,10 @@ __device__ __forceinline__ void shuffle(const Params &P, WS &w, int lane, Rng &g
 // when the shuffle cap ended the loop.
 // noline: the board is known to hold no line (the cascade loop just found
 // none), so the first line search is skipped.
-template <bool ROLL = true, class WS>
+// PRE: the next redraw's first 64 PCG outputs are evaluated before the line
+// search (they depend only on the stream position), so the jump-ahead's VALU
+// chain issues beside the search's LDS reads.
+template <bool ROLL = true, bool PRE = false, class WS>
 __device__ __forceinline__ int ensure_playable(const Params &P, WS &w, int lane, const LaneJump &J, Rng &g,
                                 const Cells<WS::NP> &cl, bool noline = false) {
     int fl = 0;
@@ -893,11 +911,17 @@ __device__ __forceinline__ int ensure_playable(const Params &P, WS &w, int lane,
         // > row + 2 unchanged, so after it no anchor lies below max(row + 2, ra).
         int lim = P.R - 1;
         for (; !noline;) {
+            DrawPre pre;
+            if constexpr (PRE) {
+                pre.sj = add128(mul128(J.Aj, U128{g.slo, g.shi}), J.incG);
+                pre.out = xsl_rr(pre.sj);
+                asm volatile("" ::"v"(pre.sj.lo), "v"(pre.sj.hi), "v"(pre.out));   // evaluate above the search
+            }
             int ra = 0;
             int r0 = first_line_row<ROLL>(P, w, lane, cl, lim, ra);
             if (r0 < 0) break;
             int row = P.R - 1 < r0 + 1 ? P.R - 1 : r0 + 1;   // colour plane only, rows 0..row
-            draw_colours(P, lane, J, g, (row + 1) * P.C, w.brd, w.trash);
+            draw_colours(P, lane, J, g, (row + 1) * P.C, w.brd, w.trash, PRE ? &pre : nullptr);
             WSYNC();
             lim = min(P.R - 1, max(row + 2, ra));
         }
@@ -913,13 +937,13 @@ __device__ __forceinline__ int ensure_playable(const Params &P, WS &w, int lane,
 }
 
 // generate_board, board.py:95-109; returns FL_ERR when a safety cap was hit
-template <bool ROLL = true, class WS>
+template <bool ROLL = true, bool PRE = false, class WS>
 __device__ __forceinline__ int generate_board(const Params &P, WS &w, int lane, const LaneJump &J, Rng &g, const Cells<WS::NP> &cl) {
     const int N = P.N;
     draw_colours(P, lane, J, g, N, w.brd, w.trash);
     for (int p = lane; p < N; p += 64) w.brd[N + p] = 1;
     WSYNC();
-    return ensure_playable<ROLL>(P, w, lane, J, g, cl) & FL_ERR;
+    return ensure_playable<ROLL, PRE>(P, w, lane, J, g, cl) & FL_ERR;
 }
 
 // Queue env e for spill_kernel; false when the queue is full.
@@ -1907,7 +1931,7 @@ __device__ __forceinline__ void reset_env(const Params &P, WS &w, int lane, int6
     const Cells<MAXN / 64> cl = make_cells<MAXN / 64>(P, lane);
     int fl;
     if constexpr (SBNB > 0) fl = sb_generate<SBNB, CODD, TMG_SB_VDET != 0>(P, w, lane, J, g, cl);   // board.py:95-109
-    else fl = generate_board<TMG_RESET_ROLL != 0>(P, w, lane, J, g, cl);
+    else fl = generate_board<TMG_RESET_ROLL != 0, TMG_RESET_PRE != 0>(P, w, lane, J, g, cl);
     note_status(P, lane, fl ? ST_INTERNAL : 0u);
     store_board(P, w, lane, board + e * 2 * N);
     store_rng(rng + e * 5, g, lane);
