@@ -705,14 +705,22 @@ __device__ __forceinline__ uint64_t bits_at(const uint64_t (&m)[NP], int start, 
 }
 
 // Returns the bottom-most row holding a line, or -1 (get_colour_lines == []).
+// lim: no anchor lies below row lim (the caller's bound).  The 64-cell passes
+// are scanned bottom-up from the one holding row lim's last cell; the scan
+// stops one pass above the first pass holding an anchor, so the masks of the
+// bottom-most anchor row rs (<= 64 cells: that pass and the one above) are
+// complete — the callers read only row rs's bits.  Unscanned passes read 0.
 template <class WS>
-__device__ __forceinline__ int detect(const Params &P, const WS &w, int lane, const Cells<WS::NP> &cl, Det<WS::NP> &d) {
+__device__ __forceinline__ int detect(const Params &P, const WS &w, int lane, const Cells<WS::NP> &cl, Det<WS::NP> &d,
+                                      int lim) {
     const int C = P.C, N = P.N, N1 = P.N - 1;
     const int8_t *col = w.brd, *typ = w.brd + N;
-    int pmax = -1;
+    const int last = min((lim + 1) * C, N) - 1;
+    int pmax = -1, stop = -2;
 #pragma unroll
-    for (int i = 0; i < WS::NP; i++) {
-        if (i * 64 >= N) { d.v[i] = 0; d.h[i] = 0; continue; }
+    for (int i = WS::NP - 1; i >= 0; i--) {
+        d.v[i] = 0; d.h[i] = 0;
+        if (i * 64 > last || i < stop) continue;                             // wave-uniform
         const int p = i * 64 + lane;
         const int pc = min(p, N1);
         const int x = col[pc];
@@ -724,7 +732,7 @@ __device__ __forceinline__ int detect(const Params &P, const WS &w, int lane, co
         d.v[i] = __ballot(vb == 0);
         d.h[i] = __ballot(hb == 0);
         const uint64_t m = d.v[i] | d.h[i];
-        if (m) pmax = i * 64 + 63 - __clzll(m);
+        if (m && pmax < 0) { pmax = i * 64 + 63 - __clzll(m); stop = i - 1; }
     }
     return pmax < 0 ? -1 : div_c(P, pmax);
 }
@@ -809,15 +817,18 @@ __device__ __forceinline__ int first_line_row(const Params &P, const WS &w, int 
 // the top).  Lanes are laid out column-major (64/R columns per pass) so one
 // ballot holds whole columns: a non-empty cell moves down by the popcount of
 // the empties below it, as one scatter.
+// cols: the columns that may hold an empty cell (bit c; others are skipped).
 template <class WS>
-__device__ __forceinline__ void gravity(const Params &P, WS &w, int lane) {
+__device__ __forceinline__ void gravity(const Params &P, WS &w, int lane, uint64_t cols = ~0ULL) {
     const int R = P.R, C = P.C, N = P.N;
     int8_t *col = w.brd, *typ = w.brd + N;
     const int cpp = 64 / R;
     const int lc = lane / R, r = lane - lc * R;
     const uint64_t colmask = (R == 64 ? ~0ULL : ((1ULL << R) - 1)) << (lc * R);
     const uint64_t above = lane == 63 ? 0ULL : ~((2ULL << lane) - 1);    // lanes > lane: lower rows
+    const uint64_t grp = cpp >= 64 ? ~0ULL : (1ULL << cpp) - 1;
     for (int c0 = 0; c0 < C; c0 += cpp) {
+        if (!((cols >> c0) & grp)) continue;                                 // wave-uniform
         const int c = c0 + lc;
         const bool in = (lc < cpp) & (c < C);
         const int p = in ? r * C + c : 0;
@@ -840,16 +851,19 @@ __device__ __forceinline__ void gravity(const Params &P, WS &w, int lane) {
 }
 
 // refill, board.py:231-241 — empties in row-major order get consecutive draws
+// rows: empties lie in rows < rows only (after gravity: the most cells
+// cleared in one column); the passes below are skipped.
 template <class WS>
-__device__ __forceinline__ void refill(const Params &P, WS &w, int lane, const LaneJump &J, Rng &g) {
+__device__ __forceinline__ void refill(const Params &P, WS &w, int lane, const LaneJump &J, Rng &g, int rows = 64) {
     const int N = P.N;
     int8_t *col = w.brd, *typ = w.brd + N;
+    const int lastp = min(rows * P.C, N);                                   // cells that may be empty
     uint64_t E[WS::NP];
     int total = 0;
 #pragma unroll
     for (int i = 0; i < WS::NP; i++) {
         int p = i * 64 + lane;
-        E[i] = __ballot(p < N && col[p] == 0 && typ[p] == 0);
+        E[i] = i * 64 < lastp ? __ballot(p < N && col[p] == 0 && typ[p] == 0) : 0ULL;
         total += __popcll(E[i]);
     }
     if (total == 0) return;
@@ -1113,7 +1127,8 @@ __device__ __forceinline__ bool plain_board(const Params &P, const WS &w, int la
 // otherwise the number of cleared cells (cleared in LDS, lasers placed,
 // SC_NNEW counted); gravity and refill are the caller's.
 template <class WS>
-__device__ __forceinline__ int simple_step_lds(const Params &P, WS &w, int lane, const Det<WS::NP> &d, int rs) {
+__device__ __forceinline__ int simple_step_lds(const Params &P, WS &w, int lane, const Det<WS::NP> &d, int rs,
+                                               uint64_t &cols, int &rows) {
     const int C = P.C, R = P.R, N = P.N, S = P.smask;
     int8_t *col = w.brd, *typ = w.brd + N;
     const uint64_t cm = C >= 64 ? ~0ULL : (1ULL << C) - 1;
@@ -1128,10 +1143,13 @@ __device__ __forceinline__ int simple_step_lds(const Params &P, WS &w, int lane,
     int vt = R;
     uint64_t vl = 0;                                                         // columns of vertical 4-lines
     bool v4 = false;
+    cols = cov | vb;
+    rows = cov ? 1 : 0;
     for (uint64_t m = vb; m; m &= m - 1) {
         const int c = __ffsll((unsigned long long)m) - 1;
         const int top = run_top(P, w, lane, rs, c);
         const int L = rs - top + 1;
+        rows = max(rows, L);
         if (L >= 5 && (S & SP_COOKIE)) return 0;
         v4 |= L == 4;
         if (L == 4 && (S & SP_VLASER)) vl |= 1ULL << c;
@@ -1612,11 +1630,19 @@ struct Serial {
 // Board.move, board.py:330-395 (the effectiveness test :352 is done by the
 // caller).  Returns eliminations; leaves the effective mask of the final
 // board in w.effw.
+// clean: the board held no line before the swap (it came out of this file's
+// ensure-playable loop), which bounds the first line search.
 template <int MAXN, bool GEN, int SBNB, bool CODD, class L>
 __device__ __forceinline__ int board_move(const Params &P, Ws<MAXN, GEN> &w, int lane, const LaneJump &J, Rng &g,
                           const Cells<MAXN / 64> &cl, int p1, int p2, int &flags, int &nn, int &na, int64_t e,
-                          L *lists) {
+                          L *lists, bool clean) {
     const int N = P.N;
+    // Bound of the bottom-most line (detect's lim): after the swap of a
+    // line-free board a line holds a swapped cell, so it is anchored at most two
+    // rows below it; after a step that cleared only cells of rows <= rs (no
+    // activation) the rows below rs are unchanged, so at most at rs + 2.
+    int lim = P.R - 1;
+    if (clean) lim = min(P.R - 1, div_c(P, max(p1, p2)) + 2);
     int8_t *col = w.brd, *typ = w.brd + N;
     int elim = 0;
     if (lane == 0) {                                                        // swap_coords :355
@@ -1643,6 +1669,7 @@ __device__ __forceinline__ int board_move(const Params &P, Ws<MAXN, GEN> &w, int
             gravity(P, w, lane);
             WSYNC();
             refill(P, w, lane, J, g);
+            lim = P.R - 1;
         } else {
             err = true;                                                     // lean variant never sees specials
         }
@@ -1666,23 +1693,28 @@ __device__ __forceinline__ int board_move(const Params &P, Ws<MAXN, GEN> &w, int
             if (!fast) {                    // bitboard step when it provably creates / activates no special
                 const int r = sb_simple_step<SBNB, CODD>(P, w, lane, J, g);
                 if (r < 0) break;
-                if (r > 0) { elim += r; iters++; continue; }
+                if (r > 0) { elim += r; iters++; lim = P.R - 1; continue; }
             }
         }
         Det<MAXN / 64> d;
-        const int rs = detect(P, w, lane, cl, d);
+        const int rs = detect(P, w, lane, cl, d, lim);
         if (rs < 0) break;
+        lim = P.R - 1;
         if (fast) {
-            elim += fast_clear(P, w, lane, cl, d, rs);
+            elim += fast_clear(P, w, lane, cl, d, rs);      // clears rows <= rs only (a deeper run would be a lower line)
+            lim = min(P.R - 1, rs + 2);
         } else {
             if constexpr (GEN && SBNB == 0) {
-                const int r = plain ? simple_step_lds(P, w, lane, d, rs) : 0;
+                uint64_t cols = 0;
+                int rows = 0;
+                const int r = plain ? simple_step_lds(P, w, lane, d, rs, cols, rows) : 0;
                 if (r > 0) {
                     elim += r;
-                    gravity(P, w, lane);
+                    gravity(P, w, lane, cols);
                     WSYNC();
-                    refill(P, w, lane, J, g);
+                    refill(P, w, lane, J, g, rows);
                     iters++;
+                    lim = min(P.R - 1, rs + 2);
                     continue;
                 }
             }
@@ -1812,7 +1844,7 @@ __device__ __forceinline__ uint32_t step_env(
     STAMP(e, 1);
     if (effective) {
         if constexpr (SBNB > 0 && !GEN) elim = sb_move<SBNB, CODD>(P, w, lane, J, g, cl, p1, p2, flags, e);
-        else elim = board_move<MAXN, GEN, SBNB, CODD, L>(P, w, lane, J, g, cl, p1, p2, flags, nn, na, e, lists);
+        else elim = board_move<MAXN, GEN, SBNB, CODD, L>(P, w, lane, J, g, cl, p1, p2, flags, nn, na, e, lists, trust_eff != 0);
         changed = true;
         if constexpr (GEN && !SPILL) {
             // the LDS lists ran out: nothing of this env has been written; queue
