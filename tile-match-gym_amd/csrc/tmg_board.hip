@@ -1076,10 +1076,12 @@ __device__ __forceinline__ int fast_clear(const Params &P, WS &w, int lane, cons
 // (:437-447), the bomb's most common row (rs) and column (the vertical's).
 // Handled when every vertical is 3 or >= 5 long (the caller's check), each run
 // meets one vertical and is at most 5 long; false otherwise.  keep: the run
-// cells that stay on the board.
-__device__ __forceinline__ bool bomb_plan(uint64_t hb, uint64_t x, uint64_t &keep) {
+// cells that stay on the board (vcols: the vertical lines' columns, whose
+// cells go with those lines); gone: the runs the bombs took.
+__device__ __forceinline__ bool bomb_plan(uint64_t hb, uint64_t x, uint64_t &keep, uint64_t vcols, uint64_t &gone) {
     const uint64_t st = hb & ~(hb << 1);                                     // run starts
     keep = 0;
+    gone = 0;
     for (uint64_t m = x; m; m &= m - 1) {
         const int c = __ffsll((unsigned long long)m) - 1;
         const uint64_t le = st & (c >= 63 ? ~0ULL : (2ULL << c) - 1);        // starts <= c
@@ -1091,7 +1093,8 @@ __device__ __forceinline__ bool bomb_plan(uint64_t hb, uint64_t x, uint64_t &kee
         if (__popcll(x & run) != 1) return false;
         const int e = s + len - 1;
         const uint64_t take = (1ULL << c) | (c > s && c < e ? (5ULL << (c - 1)) : c == s ? (3ULL << (c + 1)) : (3ULL << (c - 2)));
-        keep |= run & ~take;
+        keep |= run & ~take & ~vcols;                                        // other verticals' cells go with them
+        gone |= run;
     }
     return true;
 }
@@ -1145,11 +1148,13 @@ __device__ __forceinline__ int simple_step_lds(const Params &P, WS &w, int lane,
     bool v4 = false;
     cols = cov | vb;
     rows = cov ? 1 : 0;
+    int ptop = rs;                                                           // top row of the coords
     for (uint64_t m = vb; m; m &= m - 1) {
         const int c = __ffsll((unsigned long long)m) - 1;
         const int top = run_top(P, w, lane, rs, c);
         const int L = rs - top + 1;
         rows = max(rows, L);
+        ptop = min(ptop, top);
         if (L >= 5 && (S & SP_COOKIE)) return 0;
         v4 |= L == 4;
         if (L == 4 && (S & SP_VLASER)) vl |= 1ULL << c;
@@ -1160,11 +1165,14 @@ __device__ __forceinline__ int simple_step_lds(const Params &P, WS &w, int lane,
     const uint64_t x = vb & cov, bombc = (S & SP_BOMB) ? x : 0ULL;
     uint64_t keepc = 0;
     if (x && (hl || vl)) return 0;
-    if (bombc && (h4 || v4 || !bomb_plan(hb, bombc, keepc))) return 0;
+    uint64_t gonec = 0;
+    if (bombc && (h4 || v4 || !bomb_plan(hb, bombc, keepc, vb, gonec))) return 0;
     // coords K: lane-parallel over the cells, K = row rs's runs + the column runs
     const int th = (S & SP_HLASER) ? 3 : 2;
     bool bad = false;
-    for (int p0 = 0; p0 < N; p0 += 64) {                                    // uniform passes (bpermute)
+    // the coords lie in rows ptop..rs: only the passes holding those rows
+    const int plo = (ptop * C) & ~63, phi = min((rs + 1) * C, N);
+    for (int p0 = plo; p0 < phi; p0 += 64) {                                // uniform passes (bpermute)
         const int p = p0 + lane;
         const int r = div_c(P, p), c = p - r * C;
         const int top = __builtin_amdgcn_ds_bpermute((c & 63) << 2, vt);
@@ -1175,7 +1183,7 @@ __device__ __forceinline__ int simple_step_lds(const Params &P, WS &w, int lane,
     WSYNC();
     // get_colour_lines' perpendicular pass (:195-214): from every coord walk each
     // axis over non-coord cells of the same colour; a run of >= 3 is a line
-    for (int p = lane; p < N; p += 64) {
+    for (int p = plo + lane; p < phi; p += 64) {
         if (!w.mark[p]) continue;
         const int r = div_c(P, p), c = p - r * C, x = col[p];
         int lft = 0, rgt = 0, up = 0, dn = 0;
@@ -1189,9 +1197,9 @@ __device__ __forceinline__ int simple_step_lds(const Params &P, WS &w, int lane,
     WSYNC();
     // resolve: clear the coords (no special among them), then place the lasers
     int cleared = 0;
-    for (int p0 = 0; p0 < N; p0 += 64) {
+    for (int p0 = plo; p0 < phi; p0 += 64) {
         const int p = p0 + lane;
-        const bool k = p < N && w.mark[p];
+        const bool k = p < phi && w.mark[p];
         const int r = div_c(P, p), c = p - r * C;
         const int top = __builtin_amdgcn_ds_bpermute((c & 63) << 2, vt);
         bool pos = false, keep = false;

@@ -528,12 +528,9 @@ __device__ __forceinline__ int sb_move(const Params &P, WS &w, int lane, const L
 }
 
 // One cascade step of the general kernel (specials enabled, board.py:367-376)
-// on bitboards, when it provably reduces to the no-specials union clear:
-// get_colour_lines yields no perpendicular line, process_colour_lines
-// (:269-327) turns every first-pass line into a normal match, a laser or a
-// bomb of bomb_plan — no 5+-line when cookies are enabled, no two lines
-// sharing a cell when a laser is created — and no cleared cell holds a
-// special to activate (resolve_colour_match, :460-471).
+// on bitboards, when process_colour_lines (:269-327) makes every line a
+// normal match, a laser or a bomb of the patterns below (no cookie created)
+// and, if a matched cell holds a special, no cookie is on the board.
 // Returns -1 when there is no line, 0 when the step is not of that kind (the
 // caller runs the list machinery on the unchanged LDS board), otherwise the
 // number of cleared cells (the board in LDS has been cleared, dropped and
@@ -561,70 +558,137 @@ __device__ __forceinline__ int sb_simple_step(const Params &P, WS &w, int lane, 
     // first-pass line lengths: a horizontal run of L cells holds L-2 anchors
     const Pair h = d.ha & row;
     const Pair h2 = h & bwd<true>(h, 1);
-    const bool h4 = nonzero(andn(andn(h2, bwd<false>(h, 2)), fwd<true>(h, 1)));
     const bool h5 = nonzero(h2 & bwd<false>(h, 2));
     const Pair x4 = bwd<CODD>(bwd<false>(d.va & row, 2 * C) & eqU, C);    // 4th cell of a vertical run
-    const bool v4 = nonzero(andn(x4, eqU)), v5 = nonzero(x4 & eqU);
+    const bool v5 = nonzero(x4 & eqU);
     if ((h5 || v5) && (S & SP_COOKIE)) return 0;
-    // 4-lines become lasers (:294-302): a horizontal one an h-laser (a v-laser
-    // when only that is enabled), a vertical one a v-laser.  With no line sharing
-    // a cell, nothing is taken (:429-458) and a straight 4-line's creation cell
-    // is its second cell in (row, col) order: (rs, s+1) for a horizontal run
-    // starting at s, (top+1, c) for a vertical one.
-    const bool hl = h4 && (S & (SP_HLASER | SP_VLASER)), vl = v4 && (S & SP_VLASER);
+    const bool hlas = (S & (SP_HLASER | SP_VLASER)) != 0, vlas = (S & SP_VLASER) != 0;
     Pair kh, kv;
     sb_coords<CODD>(P, d, rs, kh, kv);
-    // lines sharing a cell: separate normal matches without bombs, bomb_plan with
-    uint64_t bombc = 0, keepc = 0;
-    if (nonzero(kh & kv)) {
-        if (hl || vl) return 0;
-        if (S & SP_BOMB) {
-            if (h4 || v4) return 0;
-            const int q = rs * C + lane;                                   // row rs as column masks
-            const uint64_t hbc = __ballot(lane < C && test(h, q));
-            bombc = __ballot(lane < C && test(kh & kv, q));
-            if (!bomb_plan(hbc, bombc, keepc)) return 0;
+    const Pair K = kh | kv;
+    const Pair inb{P.sb_in[0], P.sb_in[1]};
+    // get_colour_lines' perpendicular pass (:195-214).  On a plain board its
+    // lines are horizontal runs through a cell of a vertical line above row rs
+    // (a run through a row-rs cell, or a vertical one, would be a first-pass
+    // line of a row >= rs); X = those crossing cells.
+    const Pair eqR = andn(Pair{P.sb_nl[0], P.sb_nl[1]}, d.neR);          // same colour as the right neighbour
+    const Pair walk = andn(inb, K);
+    Pair X{0, 0};
+    {
+        const Pair nf{P.sb_nf[0], P.sb_nf[1]};
+        const Pair r1 = fwd<true>(K & eqR, 1) & walk;
+        const Pair l1 = bwd<true>(K & nf, 1) & eqR & walk;
+        if (nonzero(r1 | l1)) {
+            const Pair r2 = fwd<true>(r1 & eqR, 1) & walk;
+            const Pair l2 = bwd<true>(l1 & nf, 1) & eqR & walk;
+            X = K & (bwd<false>(r2, 2) | fwd<false>(l2, 2) | (bwd<true>(r1, 1) & fwd<true>(l1, 1)));
+        }
+        const Pair d1 = fwd<CODD>(K, C) & eqU & walk;
+        const Pair u1 = bwd<CODD>(K & eqU, C) & walk;
+        if (nonzero(d1 | u1)) {
+            const Pair d2 = fwd<CODD>(d1, C) & eqU & walk;
+            const Pair u2 = bwd<CODD>(u1 & eqU, C) & walk;
+            if (nonzero(K & (fwd<false>(u2, 2 * C) | bwd<false>(d2, 2 * C) | (fwd<CODD>(u1, C) & bwd<CODD>(d1, C)))))
+                return 0;
         }
     }
-    const Pair K = kh | kv;
-    Pair clr = K;
-    if (sb_perpendicular<CODD>(P, d, K, clr)) return 0;
+    if (nonzero(X & (row | kh))) return 0;
+    // process_colour_lines (:269-327).  Lines sort by their first coord's row
+    // (stable): a vertical before the runs crossing it and before row rs's
+    // horizontals.  A 4-line becomes a laser (:294-302; no bomb test); a vertical
+    // of 3 or >= 5 cells with bombs enabled becomes a bomb with the first line
+    // sharing a cell (:304-320) — its topmost crossing run, else the row-rs run
+    // it ends in — taking that line's two cells nearest the shared one (by
+    // distance, then column) and, the line being < 6 cells, removing it (its
+    // other cells stay).  A crossing run left in the list holds one coord, whose
+    // vertical is gone, so it is a normal match (3 cells; longer ones take the
+    // list path).  The bomb goes to the shared cell: get_special_creation_pos'
+    // corner (:437-447), the bomb's most common row and column.
+    uint64_t vcols = 0, xb = 0;                                            // vertical columns; bombs into the row-rs run
+    Pair pall{0, 0}, keep{0, 0}, pbomb{0, 0};                              // crossing runs, cells that stay, bomb cells
+    if (nonzero(X) || nonzero(kh & kv)) {
+        vcols = __ballot(lane < C && test(kv, rs * C + lane));
+        for (uint64_t m = vcols; m; m &= m - 1) {
+            const int cc = ctz64(m);
+            Pair colm;
+            if constexpr (CODD) {
+                colm = Pair{P.sb_z << ((((cc & 1) * C) + cc) >> 1), P.sb_z << ((((1 - (cc & 1)) * C) + cc) >> 1)};
+            } else {
+                colm = (cc & 1) ? Pair{0, P.sb_z << (cc >> 1)} : Pair{P.sb_z << (cc >> 1), 0};
+            }
+            colm = colm & inb;
+            const int L = popc(kv & colm);
+            const bool bomber = (S & SP_BOMB) && L != 4 && !(L >= 5 && (S & SP_COOKIE));
+            bool first = true;
+            for (Pair xc = X & colm; nonzero(xc); first = false) {
+                const int qa = xc.a ? 2 * ctz64(xc.a) : 1 << 20, qb = xc.b ? 2 * ctz64(xc.b) + 1 : 1 << 20;
+                const int q = qa < qb ? qa : qb;                           // topmost crossing left
+                if (q & 1) xc.b &= xc.b - 1; else xc.a &= xc.a - 1;
+                int lf = 0, rt = 0;
+                while (cc - lf - 1 >= 0 && test(walk, q - lf - 1) && test(eqR, q - lf - 1)) lf++;
+                while (cc + rt + 1 < C && test(walk, q + rt + 1) && test(eqR, q + rt)) rt++;
+                Pair run{0, 0};
+                for (int p = q - lf; p <= q + rt; p++) {
+                    if (p & 1) run.b |= 1ULL << (p >> 1); else run.a |= 1ULL << (p >> 1);
+                }
+                if (nonzero(run & pall)) return 0;                         // runs sharing cells
+                pall = pall | run;
+                const int len = lf + rt + 1;
+                if (bomber && first) {
+                    if (len > 5) return 0;
+                    const int t1 = lf > 0 && rt > 0 ? q - 1 : lf == 0 ? q + 1 : q - 1;
+                    const int t2 = lf > 0 && rt > 0 ? q + 1 : lf == 0 ? q + 2 : q - 2;
+                    Pair take{0, 0};
+                    for (const int p : {q, t1, t2}) {
+                        if (p & 1) take.b |= 1ULL << (p >> 1); else take.a |= 1ULL << (p >> 1);
+                    }
+                    keep = keep | andn(run, take);
+                    if (q & 1) pbomb.b |= 1ULL << (q >> 1); else pbomb.a |= 1ULL << (q >> 1);
+                } else if (len != 3) {
+                    return 0;
+                }
+            }
+            if (bomber && first && test(kh, rs * C + cc)) xb |= 1ULL << cc;
+        }
+    }
+    uint64_t keepc = 0, gonec = 0;                                         // row-rs runs a bomb took
+    if (xb) {
+        const uint64_t hbc = __ballot(lane < C && test(h, rs * C + lane));
+        if (!bomb_plan(hbc, xb, keepc, vcols, gonec)) return 0;
+    }
+    Pair clr = andn(K | pall, keep);                                       // matched cells
     const Pair sp{__ballot(y0 >= 2), __ballot(y1 >= 2)};                  // lasers / bombs
     // specials on matched cells activate (resolve_colour_match :460-471).  With
     // no cookie on the board (the only order-dependent special) the result is
     // the closure: each activated special clears its column (v-laser), row
     // (h-laser) or 3x3 (bomb) and activates the specials there (:473-525).
-    const bool act = nonzero(K & sp);
+    const bool act = nonzero(clr & sp);
     if (act && nonzero(z)) return 0;
-    // creation cells (create_special :572-597, after every activation) and the
-    // bomb runs' cells that stay
-    Pair pos{0, 0}, keep{0, 0};
+    // creation cells (create_special :572-597, after every activation): lasers
+    // at a straight 4-line's second cell in (row, col) order, (rs, s+1) for a
+    // horizontal run from s not taken by a bomb, (top+1, c) for a vertical one
+    // (nothing of theirs is taken, :429-458); bombs at their shared cell
     int8_t *ty = w.brd + N;
-    if (hl || vl) {
-        const Pair ph = hl ? fwd<true>(andn(andn(h2, bwd<false>(h, 2)), fwd<true>(h, 1)), 1) : Pair{0, 0};
-        const Pair pv = vl ? fwd<CODD>(andn(x4, eqU), C) : Pair{0, 0};
+    const int r0 = div_c(P, q0), r1 = div_c(P, q0 + 1);
+    const int c0 = q0 - rs * C, c1 = q0 + 1 - rs * C;
+    const bool in0 = r0 == rs, in1 = r1 == rs;                             // cells of row rs
+    Pair ph = hlas ? fwd<true>(andn(andn(h2, bwd<false>(h, 2)), fwd<true>(h, 1)), 1) : Pair{0, 0};
+    if (gonec) ph = andn(ph, Pair{__ballot(in0 && ((gonec >> c0) & 1)), __ballot(in1 && ((gonec >> c1) & 1))});
+    const Pair pv = vlas ? fwd<CODD>(andn(x4, eqU), C) : Pair{0, 0};
+    const Pair bombs = pbomb | Pair{__ballot(in0 && ((xb >> c0) & 1)), __ballot(in1 && ((xb >> c1) & 1))};
+    keep = keep | Pair{__ballot(in0 && ((keepc >> c0) & 1)), __ballot(in1 && ((keepc >> c1) & 1))};
+    clr = andn(clr, keep);
+    {
         const int th = (S & SP_HLASER) ? 3 : 2;
         // the lane owning the cell writes its type; sb_gravity_refill reads it back on the same lane
-        *(test(ph, q0) ? ty + q0 : w.trash + lane) = (int8_t)th;
-        *(test(ph, q0 + 1) ? ty + q0 + 1 : w.trash + 64 + lane) = (int8_t)th;
-        *(test(pv, q0) ? ty + q0 : w.trash + 128 + lane) = (int8_t)2;
-        *(test(pv, q0 + 1) ? ty + q0 + 1 : w.trash + 192 + lane) = (int8_t)2;
-        pos = ph | pv;
+        const int t0 = test(ph, q0) ? th : test(pv, q0) ? 2 : test(bombs, q0) ? 4 : 0;
+        const int t1 = test(ph, q0 + 1) ? th : test(pv, q0 + 1) ? 2 : test(bombs, q0 + 1) ? 4 : 0;
+        *(t0 ? ty + q0 : w.trash + lane) = (int8_t)t0;
+        *(t1 ? ty + q0 + 1 : w.trash + 64 + lane) = (int8_t)t1;
     }
-    if (bombc) {
-        const int r0 = div_c(P, q0), r1 = div_c(P, q0 + 1);
-        const int c0 = q0 - rs * C, c1 = q0 + 1 - rs * C;
-        const bool b0 = r0 == rs && ((bombc >> c0) & 1), b1 = r1 == rs && ((bombc >> c1) & 1);
-        const bool k0 = r0 == rs && ((keepc >> c0) & 1), k1 = r1 == rs && ((keepc >> c1) & 1);
-        *(b0 ? ty + q0 : w.trash + lane) = (int8_t)4;
-        *(b1 ? ty + q0 + 1 : w.trash + 64 + lane) = (int8_t)4;
-        pos = pos | Pair{__ballot(b0), __ballot(b1)};
-        keep = Pair{__ballot(k0), __ballot(k1)};
-    }
-    clr = andn(K, keep);                                                   // matched cells
+    const Pair pos = ph | pv | bombs;
     if (act) {
         const Pair vls{__ballot(y0 == 2), __ballot(y1 == 2)}, hls{__ballot(y0 == 3), __ballot(y1 == 3)};
-        const Pair inb{P.sb_in[0], P.sb_in[1]};
         Pair done{0, 0}, front = clr & sp;
         while (nonzero(front)) {
             const int s = front.a ? 2 * ctz64(front.a) : 2 * ctz64(front.b) + 1;

@@ -6,7 +6,7 @@
 #include "../oracle/tmg_oracle.c"
 #include <stdio.h>
 
-static long cnt[16];
+static long cnt[16], why[8];
 enum { K_SIMPLE, K_LASER, K_BOMB, K_COOKIE, K_ACT, K_ACT_LASERONLY, K_COMBO, K_ITERS, K_STEPS, K_EFF, K_PERP, K_SHARED };
 
 static int move_stats(board_t *b, int r1, int c1, int r2, int c2, long *loc) {
@@ -48,6 +48,35 @@ static int move_stats(board_t *b, int r1, int c1, int r2, int c2, long *loc) {
                 int t = b->typ[M.coords[i].c[x]];
                 if (t != 0 && t != 1) { sp = 1; if (t != T_VLASER && t != T_HLASER) sp_nonlaser = 1; }
             }
+        /* would the GPU's wave-parallel step take it? (sb_simple_step / simple_step_lds) */
+        {
+            int rs = -1, perp = 0, has4 = 0, has5 = 0, ncookie = 0;
+            for (int i = 0; i < L.n; i++) { int bot = L.v[i].c[L.v[i].n - 1] / b->C; if (bot > rs) rs = bot; }
+            for (int i = 0; i < L.n; i++) {
+                const line_t *l = &L.v[i];
+                int horiz = l->n >= 2 && l->c[0] / b->C == l->c[1] / b->C;
+                int bot = l->c[l->n - 1] / b->C;
+                if (bot != rs) perp = 1;
+                if (l->n == 4) has4 = 1;
+                if (l->n >= 5) has5 = 1;
+                (void)horiz;
+            }
+            for (int p = 0; p < b->R * b->C; p++) ncookie += b->typ[p] < 0;
+            int slow = perp || cookie || (has5 && (b->smask & 1));
+            int lasers = 0;
+            for (int i = 0; i < M.n; i++) if (M.name[i] == M_VLASER || M.name[i] == M_HLASER) lasers = 1;
+            if (shared && lasers) slow = 1;
+            if (shared && (b->smask & 8)) {
+                if (has4) slow = 1;
+                for (int i = 0; i < L.n; i++) if (L.v[i].n > 5 && L.v[i].c[0] / b->C == L.v[i].c[1] / b->C) slow = 1;
+            }
+            if (sp && (ncookie || b->R * b->C > 128)) slow = 1;
+            if (slow) loc[K_PERP]++;
+            if (slow) {
+#pragma omp atomic
+                why[perp ? 0 : cookie ? 1 : (shared && lasers) ? 2 : (shared && has4) ? 3 : sp ? 4 : 5]++;
+            }
+        }
         resolve_colour_matches(b, &M);
         loc[K_ITERS]++;
         if (shared) loc[K_SHARED]++;
@@ -98,7 +127,8 @@ int main(int argc, char **argv) {
 #pragma omp critical
         for (int i = 0; i < 16; i++) cnt[i] += loc[i];
     }
-    const char *nm[] = {"simple", "laser", "bomb", "cookie", "activation", "act_laser_only", "combo", "iters", "steps", "effective", "perp", "shared"};
+    const char *nm[] = {"simple", "laser", "bomb", "cookie", "activation", "act_laser_only", "combo", "iters", "steps", "effective", "serial(est)", "shared"};
     for (int i = 0; i < 12; i++) printf("%-15s %10ld  %.4f per iter\n", nm[i], cnt[i], cnt[K_ITERS] ? (double)cnt[i] / cnt[K_ITERS] : 0.0);
+    printf("serial reasons: perp %ld cookie %ld shared+laser %ld shared+4line(bomb) %ld act+cookie %ld other %ld\n", why[0], why[1], why[2], why[3], why[4], why[5]);
     return 0;
 }
