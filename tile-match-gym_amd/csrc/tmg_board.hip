@@ -576,8 +576,9 @@ __device__ __forceinline__ bool eff_exact(const Params &P, const int8_t *brd, in
     return false;
 }
 
-// is_move_effective for every action of a clean board (no cookie, no
-// pre-existing colour triple, checked by the caller): only triples through
+// is_move_effective for every action of a clean board (no empty cell, no
+// coloured cookie, no pre-existing colour triple, checked by the caller; a
+// swap with a colourless cookie is effective by type): only triples through
 // exactly one of the two swapped cells can appear, all inside the window.  Pass i
 // takes vertical action i and horizontal action nv + i on every lane; within
 // a direction each swapped pair's 14 neighbours sit at the same offsets (±1,
@@ -618,8 +619,11 @@ __device__ __forceinline__ bool scan_effective_clean(const Params &P, WS &w, int
             const uint32_t hq = umin3(nq(col[q + C], x1, neg(R - 3 - r)) | nq(col[q + 2 * C], x1, neg(R - 4 - r)),
                                       nq(col[q - 1], x1, l1) | umin(nq(col[q - 2], x1, l2), nq(col[q + 1], x1, g1)),
                                       nq(col[q + 1], x1, g1) | nq(col[q + 2], x1, g2));
-            uint32_t sp = 1u;                                // 0 iff both are specials (type not in {0, 1})
-            if constexpr (TYPES) sp = umin((uint32_t)(int)typ[p], (uint32_t)(int)typ[q]) > 1u ? 0u : 1u;
+            uint32_t sp = 1u;            // 0 iff both are specials (type not in {0, 1}) or one is a cookie (type < 0)
+            if constexpr (TYPES) {
+                const uint32_t tp = (uint32_t)(int)typ[p], tq = (uint32_t)(int)typ[q];
+                sp = (umin(tp, tq) > 1u || ((tp | tq) >> 31)) ? 0u : 1u;
+            }
             fv = umin3(sp, hp, hq) | neg(nv - 1 - i);
         }
         {   // horizontal action nv + i: i = r*(C-1) + c, p = r*C + c, q = p + 1
@@ -635,7 +639,10 @@ __device__ __forceinline__ bool scan_effective_clean(const Params &P, WS &w, int
                                       nq(col[q - C], x1, u1) | umin(nq(col[q - 2 * C], x1, u2), nq(col[q + C], x1, d1)),
                                       nq(col[q + C], x1, d1) | nq(col[q + 2 * C], x1, d2));
             uint32_t sp = 1u;
-            if constexpr (TYPES) sp = umin((uint32_t)(int)typ[p], (uint32_t)(int)typ[q]) > 1u ? 0u : 1u;
+            if constexpr (TYPES) {
+                const uint32_t tp = (uint32_t)(int)typ[p], tq = (uint32_t)(int)typ[q];
+                sp = (umin(tp, tq) > 1u || ((tp | tq) >> 31)) ? 0u : 1u;
+            }
             fh = umin3(sp, hp, hq) | neg(nh - 1 - i);
         }
         const uint64_t mv = __ballot(fv == 0u), mh = __ballot(fh == 0u);
@@ -658,13 +665,17 @@ __device__ __forceinline__ bool scan_effective(const Params &P, WS &w, int lane,
     const int8_t *col = w.brd, *typ = w.brd + N;
     bool exact = false;
     if (!clean) {
-        bool odd = false;      // cookie on board or a pre-existing triple -> exact scan
+        // an empty cell, a cookie that gained a colour or a pre-existing triple ->
+        // exact scan.  Colourless cookies are fine: swapping one is effective
+        // (board.py:752-753), and colour 0 matches no coloured tile; a cookie
+        // triple does not count (its third cell's type is < 0, :763).
+        bool odd = false;
 #pragma unroll
         for (int i = 0; i < WS::NP; i++) {
             int p = i * 64 + lane;
             if (p < N) {
                 int r = cl.r(i), c = cl.c(i), x = col[p];
-                odd |= typ[p] < 0;
+                odd |= typ[p] == 0 || (typ[p] < 0 && x != 0);
                 odd |= (c + 2 < C) && col[p + 1] == x && col[p + 2] == x && typ[p + 2] >= 0;
                 odd |= (r + 2 < R) && col[p + C] == x && col[p + 2 * C] == x && typ[p + 2 * C] >= 0;
             }

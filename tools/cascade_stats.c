@@ -97,6 +97,14 @@ static int move_stats(board_t *b, int r1, int c1, int r2, int c2, long *loc) {
         get_colour_lines(b, &L);
     }
     lines_free(&L);
+    {
+        int ck = 0;
+        for (int p = 0; p < b->R * b->C; p++) ck |= b->typ[p] < 0;
+        if (ck) {
+#pragma omp atomic
+            why[6]++;
+        }
+    }
     return 0;
 }
 
@@ -129,6 +137,6 @@ int main(int argc, char **argv) {
     }
     const char *nm[] = {"simple", "laser", "bomb", "cookie", "activation", "act_laser_only", "combo", "iters", "steps", "effective", "serial(est)", "shared"};
     for (int i = 0; i < 12; i++) printf("%-15s %10ld  %.4f per iter\n", nm[i], cnt[i], cnt[K_ITERS] ? (double)cnt[i] / cnt[K_ITERS] : 0.0);
-    printf("serial reasons: perp %ld cookie %ld shared+laser %ld shared+4line(bomb) %ld act+cookie %ld other %ld\n", why[0], why[1], why[2], why[3], why[4], why[5]);
+    printf("serial reasons: perp %ld cookie %ld shared+laser %ld shared+4line(bomb) %ld act+cookie %ld other %ld; effective moves ending with a cookie on the board %ld\n", why[0], why[1], why[2], why[3], why[4], why[5], why[6]);
     return 0;
 }
