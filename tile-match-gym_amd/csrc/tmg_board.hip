@@ -769,7 +769,8 @@ __device__ __forceinline__ int run_top(const Params &P, const WS &w, int lane, i
 // one holding row lim's last cell upwards and the scan stops one pass above
 // the first pass holding an anchor: the bottom-most anchor row (C <= 64
 // cells) lies in that pass and the one above it.  ra: the anchor row found.
-template <bool ROLL, class WS>
+// ALL1: every type is 1 (generate_board's loop), so the type plane is not read.
+template <bool ROLL, bool ALL1 = false, class WS>
 __device__ __forceinline__ int first_line_row(const Params &P, const WS &w, int lane, const Cells<WS::NP> &cl,
                                               int lim, int &ra) {
     const int C = P.C, N = P.N, N1 = P.N - 1;
@@ -785,7 +786,7 @@ __device__ __forceinline__ int first_line_row(const Params &P, const WS &w, int 
             const int x = col[pc];
             const int u1 = col[max(pc - C, 0)], u2 = col[max(pc - 2 * C, 0)];
             const int h1 = col[min(pc + 1, N1)], h2 = col[min(pc + 2, N1)];
-            const uint32_t tbad = (uint32_t)((int)typ[pc] - 1) >> 31;
+            const uint32_t tbad = ALL1 ? 0u : (uint32_t)((int)typ[pc] - 1) >> 31;
             const uint32_t vb = cl.vbad(i) | tbad | ne(u1, x) | ne(u2, x);
             const uint32_t hb = cl.hbad(i) | tbad | ne(h1, x) | ne(h2, x);
             const int base = cl.key(i);
@@ -806,7 +807,7 @@ __device__ __forceinline__ int first_line_row(const Params &P, const WS &w, int 
             const int x = col[pc];
             const int u1 = col[max(pc - C, 0)], u2 = col[max(pc - 2 * C, 0)];
             const int h1 = col[min(pc + 1, N1)], h2 = col[min(pc + 2, N1)];
-            const uint32_t tbad = (uint32_t)((int)typ[pc] - 1) >> 31;
+            const uint32_t tbad = ALL1 ? 0u : (uint32_t)((int)typ[pc] - 1) >> 31;
             const uint32_t vbad = (p < N && r >= 2) ? 0u : 1u, hbad = (p < N && c + 2 < C) ? 0u : 1u;
             const uint32_t vb = vbad | tbad | ne(u1, x) | ne(u2, x);
             const uint32_t hb = hbad | tbad | ne(h1, x) | ne(h2, x);
@@ -927,7 +928,7 @@ __device__ __forceinline__ void shuffle(const Params &P, WS &w, int lane, Rng &g
 // PRE: the next redraw's first 64 PCG outputs are evaluated before the line
 // search (they depend only on the stream position), so the jump-ahead's VALU
 // chain issues beside the search's LDS reads.
-template <bool ROLL = true, bool PRE = false, class WS>
+template <bool ROLL = true, bool PRE = false, bool ALL1 = false, class WS>
 __device__ __forceinline__ int ensure_playable(const Params &P, WS &w, int lane, const LaneJump &J, Rng &g,
                                 const Cells<WS::NP> &cl, bool noline = false) {
     int fl = 0;
@@ -943,7 +944,7 @@ __device__ __forceinline__ int ensure_playable(const Params &P, WS &w, int lane,
                 asm volatile("" ::"v"(pre.sj.lo), "v"(pre.sj.hi), "v"(pre.out));   // evaluate above the search
             }
             int ra = 0;
-            int r0 = first_line_row<ROLL>(P, w, lane, cl, lim, ra);
+            int r0 = first_line_row<ROLL, ALL1>(P, w, lane, cl, lim, ra);
             if (r0 < 0) break;
             int row = P.R - 1 < r0 + 1 ? P.R - 1 : r0 + 1;   // colour plane only, rows 0..row
             draw_colours(P, lane, J, g, (row + 1) * P.C, w.brd, w.trash, PRE ? &pre : nullptr);
@@ -968,7 +969,7 @@ __device__ __forceinline__ int generate_board(const Params &P, WS &w, int lane, 
     draw_colours(P, lane, J, g, N, w.brd, w.trash);
     for (int p = lane; p < N; p += 64) w.brd[N + p] = 1;
     WSYNC();
-    return ensure_playable<ROLL, PRE>(P, w, lane, J, g, cl) & FL_ERR;
+    return ensure_playable<ROLL, PRE, true>(P, w, lane, J, g, cl) & FL_ERR;         // types all 1
 }
 
 // Queue env e for spill_kernel; false when the queue is full.
