@@ -289,7 +289,10 @@ struct ListStore {
 #ifndef TMG_CAP128
 #define TMG_CAP128 64         // lane-0 list capacity of the <= 128-cell general kernels (cells; more spills)
 #endif
-template <int MAXN, int CAP = (MAXN > 128 ? MAXN / 2 : TMG_CAP128)>
+#ifndef TMG_CAP512
+#define TMG_CAP512 128        // lane-0 list capacity of the 512-cell general kernels (cells; overflow -> spill path)
+#endif
+template <int MAXN, int CAP = (MAXN > 128 ? TMG_CAP512 : TMG_CAP128)>
 using WsSerial = ListStore<4 * CAP + 256, CAP + 64, 2 * CAP + 64, CAP + 32, 4 * CAP + 256, CAP + 8>;
 
 // Global-memory lists sized at the worst case of any board of <= MAXN cells
