@@ -69,7 +69,7 @@ namespace tmg {
 #define TMG_RQ128_WAVES 5      // min waves per SIMD for the 128-cell reset-queue kernel (87 VGPRs, no spill)
 #endif
 #ifndef TMG_RESET512_WAVES
-#define TMG_RESET512_WAVES 4   // min waves per SIMD for the 512-cell reset kernel (caps its VGPRs)
+#define TMG_RESET512_WAVES 5   // min waves per SIMD for the 512-cell reset kernel (caps its VGPRs; A/B 4 / 6 slower)
 #endif
 
 // compiler-only ordering point between a wave's LDS loads and later stores
