@@ -62,6 +62,9 @@ namespace tmg {
 #ifndef TMG_RESET_PRE
 #define TMG_RESET_PRE 1        // the 512-cell reset kernel evaluates each redraw's first PCG batch before its line search
 #endif
+#ifndef TMG_GEN512_WAVES
+#define TMG_GEN512_WAVES TMG_WPE   // min waves per SIMD for the 512-cell general step kernel (0: compiler's choice, 3)
+#endif
 #ifndef TMG_LEAN128_WAVES
 #define TMG_LEAN128_WAVES TMG_WPE   // min waves per SIMD for the <= 128-cell lean step kernels (c2)
 #endif
@@ -1920,7 +1923,7 @@ __device__ __forceinline__ uint32_t step_env(
 
 // TileMatchEnv.step over a batch, one wave per env.
 template <int MAXN, bool GEN, int SBNB = 0, bool CODD = false>
-__global__ __launch_bounds__(64 * TMG_WPB, MAXN == 128 ? (GEN ? TMG_GEN128_WAVES : TMG_LEAN128_WAVES) : TMG_WPE) void step_kernel(
+__global__ __launch_bounds__(64 * TMG_WPB, MAXN == 128 ? (GEN ? TMG_GEN128_WAVES : TMG_LEAN128_WAVES) : (GEN ? TMG_GEN512_WAVES : TMG_WPE)) void step_kernel(
     Params P, int64_t n, int8_t *__restrict__ board, uint64_t *__restrict__ rng, int32_t *__restrict__ timer,
     const int32_t *__restrict__ actions, int32_t *__restrict__ reward, int32_t *__restrict__ n_new,
     int32_t *__restrict__ n_act, uint8_t *__restrict__ flags_out, uint64_t *__restrict__ eff, int trust_eff,
