@@ -16,6 +16,9 @@ are regenerated (tile_match_env.py:84-91 -> board.py:95-131), so any timed
 window of a multiple of 10 steps (the driver's 20, the default 300) holds
 exactly its share of the reset work (20 steps: 2/3 of the boards), and each
 block's regeneration overlaps the other groups' steps on their streams.
+`--phase-align 1` (default) moves that schedule so the timed window opens on a
+block's reset step: same reset work per window, but no reset right before the
+window's end, whose regeneration tail would then have nothing to overlap.
 P = 1 is the aligned run (every env resets on the same step); P = 0 staggers
 every env (env i at timer i mod 30: each step regenerates N/30 boards, and the
 step time is then the slowest of those regenerations).
@@ -172,6 +175,9 @@ def main():
     ap.add_argument("--phase-blocks", type=int, default=3,
                     help="episode phase blocks: P contiguous env blocks offset by 30/P steps (1 = aligned, "
                          "0 = every env staggered)")
+    ap.add_argument("--phase-align", type=int, default=1,
+                    help="1: shift the phase blocks so the timed window opens on a block's reset step (0: phases "
+                         "from step 0)")
     ap.add_argument("--phase-interleave", action="store_true",
                     help="env i in phase block i mod P (every env group holds all blocks) instead of contiguous blocks")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -210,8 +216,17 @@ def main():
     T = 300
     acts = torch.from_numpy(synthetic_actions(rng_, T, A)).to(dev)
     env.reset()
+    # --phase-align: move the reset schedule so that the timed window opens on a
+    # block's reset step (the blocks' resets are `spacing` steps apart; any
+    # window of a multiple of `spacing` steps holds the same reset work however
+    # it is aligned, but one ending just after a reset times that reset's tail
+    # with nothing left to overlap it)
+    spacing = moves // max(1, args.phase_blocks)
+    shift = (moves - 1 - args.warmup) % spacing if (args.phase_align and args.phase_blocks > 1
+                                                    and not args.phase_interleave) else 0
     if args.phase_blocks != 1:
-        env.stagger_phases(blocks=args.phase_blocks, first_env=rng_.start, interleave=args.phase_interleave)
+        env.stagger_phases(blocks=args.phase_blocks, first_env=rng_.start, interleave=args.phase_interleave,
+                           shift=shift)
     env.status(clear=True)
 
     def step(t):
@@ -295,7 +310,9 @@ def main():
                                    + (", episodes aligned" if args.phase_blocks == 1 else
                                       ", every env's episode phase staggered (timer0 = env mod 30)" if args.phase_blocks <= 0
                                       else f", {args.phase_blocks} episode-phase blocks offset by "
-                                           f"{moves // args.phase_blocks} steps")
+                                           f"{moves // args.phase_blocks} steps"
+                                           + (f", the timed window opening on a block's reset step (phases + {shift})"
+                                              if shift else ""))
                                    + ("" if args.policy == "uniform" else ", effective-action policy"),
                        "boards_per_gpu": nb, "rows": R, "cols": C, "colours": k,
                        "specials": cl + co, "env_groups_per_gpu": env.groups,

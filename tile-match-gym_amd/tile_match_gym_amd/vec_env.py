@@ -115,7 +115,7 @@ class TileMatchVecEnv:
         w = batch_rng_words(seeds)
         self.rng.copy_(torch.from_numpy(w.view(np.int64)))
 
-    def stagger_phases(self, blocks: int = 0, first_env: int = 0, interleave: bool = False):
+    def stagger_phases(self, blocks: int = 0, first_env: int = 0, interleave: bool = False, shift: int = 0):
         """Offset the episode phases right after a reset by setting timers.  A
         timer of m is the state after m ineffective moves (board.py:352-353: no
         board or RNG change; tile_match_env.py:100 counts the move).
@@ -130,7 +130,10 @@ class TileMatchVecEnv:
         groups take turns, so a window of a multiple of M / Pg steps holds the
         same reset work on every group's stream.
         interleave=True: env i belongs to block i mod P instead, so every group
-        stream holds an equal part of every block's resets."""
+        stream holds an equal part of every block's resets.
+        shift: every phase advanced by `shift` steps (mod num_moves), i.e. the
+        whole reset schedule moved `shift` steps earlier; the reset work per
+        window of a multiple of the block spacing is unchanged."""
         self.join()
         N, M = self.num_envs, self.num_moves
         if blocks == 1:
@@ -148,7 +151,7 @@ class TileMatchVecEnv:
                 n = hi - lo
                 for j in range(Pg):
                     a, b = lo + j * n // Pg, lo + (j + 1) * n // Pg
-                    t[a:b] = (j * M // Pg + g * M // (Pg * G)) % M
+                    t[a:b] = (j * M // Pg + g * M // (Pg * G) + shift) % M
             self.timer.copy_(t.to(torch.int32).to(self.device))
         else:
             g = torch.arange(first_env, first_env + N, device=self.device, dtype=torch.int64)
