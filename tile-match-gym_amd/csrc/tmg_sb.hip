@@ -247,7 +247,10 @@ __device__ __forceinline__ void sb_coords(const Params &P, const SBDet &d, int r
 // get_colour_lines' perpendicular pass (board.py:195-214): from every coord of K
 // walk each axis over non-coord cells of the same colour; a run of >= 3 is a
 // line.  Adds the cells of those lines to clr; returns whether there is one.
-template <bool CODD>
+// On a board of type-1 tiles (the lean path) only the horizontal part can find
+// a line: a vertical run through a coord would extend a first-pass vertical or
+// be anchored below row rs (HORIZ_ONLY skips it).
+template <bool CODD, bool HORIZ_ONLY = false>
 __device__ __forceinline__ bool sb_perpendicular(const Params &P, const SBDet &d, const Pair K, Pair &clr) {
     const int C = P.C;
     const Pair inb{P.sb_in[0], P.sb_in[1]};
@@ -271,6 +274,7 @@ __device__ __forceinline__ bool sb_perpendicular(const Params &P, const SBDet &d
             while (nonzero(g)) { clr = clr | g; g = bwd<true>(g & nf, 1) & eqR & walk; }
         }
     }
+    if constexpr (HORIZ_ONLY) return any;
     // vertical runs through coords
     const Pair d1 = fwd<CODD>(K, C) & eqU & walk;
     const Pair u1 = bwd<CODD>(K & eqU, C) & walk;
@@ -297,7 +301,7 @@ __device__ __forceinline__ Pair sb_clear(const Params &P, const SBDet &d, int rs
     sb_coords<CODD>(P, d, rs, kh, kv);
     const Pair K = kh | kv;
     Pair clr = K;
-    sb_perpendicular<CODD>(P, d, K, clr);
+    sb_perpendicular<CODD, true>(P, d, K, clr);
     return clr;
 }
 
