@@ -208,7 +208,9 @@ def main():
     torch.cuda.set_device(local_rank % max(1, ndev))
     dev = torch.device("cuda", torch.cuda.current_device())
 
+    from tile_match_gym_amd import _native
     from tile_match_gym_amd.vec_env import TileMatchVecEnv
+    build = _native.build_info()            # the loader has checked the library against this tree's sources
     moves = 30
     env = TileMatchVecEnv(nb, R, C, k, moves, cl, co, seeds=shard_seeds(rank, nb), device=dev, autoreset=True,
                           groups=args.groups)
@@ -326,6 +328,7 @@ def main():
                          "per_launch_gbs": round(bpu * launch_envs / (kern_ms * 1e-3) / 1e9, 2),
                          "issue": issue},
             "cpu_baseline": cpu,
+            "build": {k: (v[:16] if k in ("src", "so_sha256") else v) for k, v in build.items() if k != "path"},
         }
         print(json.dumps(out), flush=True)
     if dist:

@@ -20,10 +20,12 @@
  *   n_new  int32 [n]   info["num_new_specials"]
  *   n_act  int32 [n]   info["num_specials_activated"]
  *   flags  uint8 [n]   bit0 done, bit1 is_combination_match, bit2 shuffled,
- *                      bit3 autoreset ran, bit6 capacity overflow (more than
- *                      4096 envs of one launch outgrew the LDS lists at once:
- *                      that step is not exact), bit7 error (step after done /
- *                      bad action, or an internal safety cap) tile_match_env.py:94-95
+ *                      bit3 autoreset ran, bit7 error (step after done / bad
+ *                      action, or an internal safety cap)  tile_match_env.py:94-95
+ *                      (bit6, capacity overflow, is no longer produced: a step
+ *                      whose cascade outgrows the kernels' LDS lists is re-run
+ *                      on worst-case lists, and the queue of such steps holds
+ *                      every env of the launch)
  *
  * Errors: 0 = ok, negative = error; tmg_last_error() gives a thread-local
  * message.  All launches are asynchronous on `stream` (a hipStream_t; NULL =
@@ -32,6 +34,7 @@
 #ifndef TMG_H
 #define TMG_H
 
+#include <stddef.h>
 #include <stdint.h>
 
 #ifdef __cplusplus
@@ -56,7 +59,7 @@ typedef struct tmg_ctx tmg_ctx;
 #define TMG_FLAG_COMBO     0x02u
 #define TMG_FLAG_SHUFFLED  0x04u
 #define TMG_FLAG_RESET     0x08u
-#define TMG_FLAG_OVERFLOW  0x40u
+#define TMG_FLAG_OVERFLOW  0x40u   /* not produced since ABI 3 (kept for old callers) */
 #define TMG_FLAG_ERROR     0x80u
 
 /* Replaces TileMatchEnv.__init__ / Board.__init__ (tile_match_env.py:17-77,
@@ -65,6 +68,13 @@ typedef struct tmg_ctx tmg_ctx;
  * jump-ahead table on `device`. */
 TMG_API int tmg_create(tmg_ctx **out, int device, int rows, int cols, int colours,
                uint32_t specials_mask, int num_moves);
+
+/* A context for tmg_effective only, on any rows x cols board of up to 512
+ * cells (no viability test, no colours or specials): the module-level
+ * is_move_effective(board, c1, c2) / Board.possible_move(grid) of the
+ * reference (board.py:558-569, 735-787), which accept any board.  Every other
+ * call on it fails. */
+TMG_API int tmg_create_scan(tmg_ctx **out, int device, int rows, int cols);
 
 /* Frees the context's device tables.  Never frees caller buffers. */
 TMG_API int tmg_destroy(tmg_ctx *ctx);
@@ -78,9 +88,11 @@ TMG_API int tmg_reset(tmg_ctx *ctx, int64_t n, int8_t *board, uint64_t *rng, int
 
 /* Replaces TileMatchEnv.step (tile_match_env.py:93-112 -> Board.move,
  * board.py:330-395) for n envs at once.  actions[i] in [0, A).
- * trust_eff != 0: eff holds the mask this library produced for the current
- *   boards (the effectiveness test of board.py:352 is then a bit lookup);
- *   pass 0 after editing boards by hand.
+ * trust_eff != 0: eff holds the mask a tmg_step / tmg_reset of this library
+ *   wrote for the current boards (the effectiveness test of board.py:352 is
+ *   then a bit lookup, and the boards are known to hold no line, which bounds
+ *   the first line search); pass 0 after editing boards by hand, also when the
+ *   mask was then recomputed by tmg_effective.
  * autoreset != 0: an env whose episode ends is regenerated in the same call
  *   (continuing its RNG stream, == reset() without a seed); reward / flags
  *   still describe the final move and flag bit3 is set.  With autoreset == 0
@@ -143,8 +155,8 @@ TMG_API int tmg_count_states(int device, int rows, int cols, int colours, uint64
 
 /* Sticky status of the context: the OR, over every env of every call since
  * the last clear, of TMG_STATUS_INTERNAL (a safety cap or an inconsistent
- * board ended a step with TMG_FLAG_ERROR), TMG_STATUS_OVERFLOW (a step met
- * TMG_FLAG_OVERFLOW) and TMG_STATUS_CALLER (a step after done / a bad action).
+ * board ended a step with TMG_FLAG_ERROR), TMG_STATUS_OVERFLOW (not produced
+ * since ABI 3) and TMG_STATUS_CALLER (a step after done / a bad action).
  * Waits for the device; clear != 0 then zeroes it.  The reference raises at
  * the point of failure (tile_match_env.py:94-95, board.py:349-350); a batch
  * reports through this word and the per-env flags instead. */
@@ -155,7 +167,8 @@ TMG_API int tmg_status(tmg_ctx *ctx, uint32_t *status, int clear);
 
 /* Number of steps, since the context was created, whose cascade outgrew the
  * general kernels' LDS lists and was re-run on global-memory lists sized for
- * the worst case (spill_kernel; diagnostic — results are exact either way).
+ * the worst case (spill_kernel; diagnostic — results are exact either way;
+ * the queue of such steps is sized per stream for the largest launch).
  * Waits for the device. */
 TMG_API int tmg_spills(tmg_ctx *ctx, uint64_t *count);
 
@@ -173,6 +186,11 @@ TMG_API const char *tmg_last_error(void);
 
 /* ABI version (bumped on any signature change). */
 TMG_API int tmg_abi_version(void);
+
+/* "src=<sha256 of the library's sources>;variant=<product|diagnostic name>":
+ * the loader compares the hash with the sources next to the library and
+ * refuses a stale build. */
+TMG_API const char *tmg_build_info(void);
 
 #ifdef __cplusplus
 }

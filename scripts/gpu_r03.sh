@@ -1,0 +1,46 @@
+#!/bin/bash
+# Round-3 GPU evidence.  Usage (through gpurun, from the repo root):
+#   STAGE=tests bash scripts/gpu_r03.sh   # pytest -m gpu (all but the deep rollouts), smoke, c2 bench
+#   STAGE=deep  bash scripts/gpu_r03.sh   # the deep rollouts vs the oracle + the TMG_COVER branch counts
+#   STAGE=bench bash scripts/gpu_r03.sh   # c2 / c3 / c5 bench lines with the CPU baseline + driver window
+#   STAGE=prof  bash scripts/gpu_r03.sh   # rocprofv3 --kernel-trace --stats of the c2 / c3 / c5 benches
+# Each GPU step has its own time limit; the script stops at the first failure.
+cd "${GRAFT_REPO_ROOT:-/root/repo}"
+TAG=${TAG:-r03}
+OUT=gpurun_out/$TAG
+mkdir -p $OUT
+export TMPDIR=/tmp
+PYT="python -u -m pytest -x -v --timeout 240 --timeout-method thread"
+case "${STAGE:-tests}" in
+tests)
+  TMG_EVIDENCE_DIR=$OUT/evidence timeout -k 10 900 $PYT tests -m gpu --ignore=tests/test_gpu_deep.py \
+    > $OUT/pytest_gpu.log 2>&1 || { echo "pytest failed"; tail -30 $OUT/pytest_gpu.log; exit 1; }
+  tail -1 $OUT/pytest_gpu.log
+  timeout -k 10 200 python -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1 \
+    || { echo "smoke failed"; tail -5 $OUT/smoke.log; exit 1; }
+  cat $OUT/smoke.log
+  timeout -k 10 300 python bench.py --no-cpu-baseline > $OUT/c2_bench.log 2>&1 || { echo "bench failed"; tail $OUT/c2_bench.log; exit 1; }
+  tail -1 $OUT/c2_bench.log | cut -c1-300
+  ;;
+deep)
+  TMG_COVER_OUT=$OUT/cover.json timeout -k 10 1000 $PYT tests/test_gpu_deep.py > $OUT/pytest_deep.log 2>&1 \
+    || { echo "deep failed"; tail -30 $OUT/pytest_deep.log; exit 1; }
+  tail -3 $OUT/pytest_deep.log
+  ;;
+bench)
+  for c in c2 c3 c5; do
+    timeout -k 10 400 python bench.py --config $c > $OUT/${c}_bench.log 2>&1 || { echo "bench $c failed"; tail $OUT/${c}_bench.log; exit 1; }
+    tail -1 $OUT/${c}_bench.log | cut -c1-200
+  done
+  timeout -k 10 300 python bench.py --steps 20 --warmup 5 --no-cpu-baseline > $OUT/c2_driver_window_bench.log 2>&1 || exit 1
+  tail -1 $OUT/c2_driver_window_bench.log | cut -c1-200
+  ;;
+prof)
+  for c in c2 c3 c5; do
+    timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $OUT/prof_$c -o run --output-format csv -- \
+      python3 bench.py --config $c --steps 90 --warmup 30 --no-cpu-baseline > $OUT/${c}_prof_bench.log 2>&1 \
+      || { echo "prof $c failed"; tail $OUT/${c}_prof_bench.log; exit 1; }
+    tail -1 $OUT/${c}_prof_bench.log | cut -c1-200
+  done
+  ;;
+esac

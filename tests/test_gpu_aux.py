@@ -113,6 +113,7 @@ def test_vector_env_autoreset_modes(mode):
     ref.reset()
     assert np.array_equal(obs["board"].cpu().numpy(), ref.board.astype(np.int32))
     A = venv.single_action_space.n
+    assert venv.action_space.shape == (venv.num_envs,) and (venv.action_space.nvec == A).all()
     rs = np.random.default_rng(1)
     pending = np.zeros(n, bool)
     for t in range(3 * moves + 2):
@@ -240,3 +241,47 @@ def test_checkpoint_restore_vs_oracle(tmp_path):
         assert np.array_equal(env2.reward.cpu().numpy(), o.reward), t
         assert np.array_equal(env2.flags.cpu().numpy(), o.flags), t
         assert np.array_equal(env2.eff.cpu().numpy().view(np.uint64), o.eff), t
+
+
+@pytest.mark.parametrize("R,C,k,sm", [(10, 10, 4, 0), (10, 10, 4, 14), (20, 20, 6, 15)])
+def test_step_effective_after_hand_edit_with_low_line(R, C, k, sm):
+    """Boards edited by hand to hold a line in their bottom row, the mask
+    invalidated, then TileMatchVecEnv.step_effective: the policy samples from
+    tmg_effective's mask, and that step must run untrusted — a mask from
+    tmg_effective says nothing about lines already on the board, which the
+    reference's cascade clears first (board.py:367-391: get_colour_lines scans
+    from the bottom).  Every field equals the oracle for that step and the
+    next ones."""
+    from oracle.policy_np import sample_effective_np
+    from tile_match_gym_amd.vec_env import TileMatchVecEnv
+    cl, co = _lists(sm)
+    n = 2048
+    env = TileMatchVecEnv(n, R, C, k, 30, cl, co, seed=61, device=DEV)
+    o = orc.OracleBatch(R, C, k, sm, 30, env.rng_words().copy(), threads=16)
+    env.reset()
+    o.reset()
+    b = env.board.cpu().numpy()
+    rs = np.random.default_rng(3)
+    for i in range(n):                                  # a horizontal 3-line of normals low on the board
+        r = R - 1 - int(rs.integers(0, 2))
+        c = int(rs.integers(0, C - 2))
+        b[i, 0, r, c:c + 3] = 1 + int(rs.integers(0, k))
+        b[i, 1, r, c:c + 3] = 1
+    env.board.copy_(torch.from_numpy(b))
+    o.board[:] = b
+    env.invalidate_effective_cache()
+    A = env.num_actions
+    for i in range(n):                                   # the oracle's view of the edited boards' masks
+        m, _ = orc.effective_mask(b[i])
+        o.eff[i] = np.packbits(np.concatenate([m, np.zeros(o.W * 64 - A, bool)]), bitorder="little").view(np.uint64)
+    for t in range(4):
+        a = sample_effective_np(o.eff, A, 4242, 0, t)
+        env.step_effective(t, key=4242)
+        env.join()
+        o.step(a, autoreset=True)
+        assert np.array_equal(env.actions.cpu().numpy(), a), t
+        for f in ("board", "reward", "n_new", "n_act", "flags", "timer"):
+            assert np.array_equal(getattr(env, f).cpu().numpy(), getattr(o, f)), (t, f)
+        assert np.array_equal(env.rng_words(), o.rng), t
+        assert np.array_equal(env.eff.cpu().numpy().view(np.uint64), o.eff), t
+    assert env.status() == 0

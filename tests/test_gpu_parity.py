@@ -247,34 +247,3 @@ def test_bench_phase_stagger_vs_oracle(blocks, R, C, k, sm):
     assert np.array_equal(env.rng_words(), ref.rng)
     assert np.array_equal(env.timer.cpu().numpy(), ref.timer)
     assert env.status() == 0
-
-
-@pytest.mark.parametrize("R,C,k,sm", [(10, 10, 4, 14), (20, 20, 6, 15)])
-def test_reset_queue_option_vs_oracle(R, C, k, sm, monkeypatch):
-    """TMG_RESETQ=1: deferred autoresets drained from the per-stream queue
-    (reset_queue_kernel) instead of the FL_RESET-masked launch — same
-    trajectories as the oracle, aligned episodes (a whole-batch reset) and
-    staggered ones (a few resets per step)."""
-    from tile_match_gym_amd.shard import synthetic_actions
-    from tile_match_gym_amd.vec_env import TileMatchVecEnv
-    monkeypatch.setenv("TMG_RESETQ", "1")
-    cl = ["cookie"] if sm & 1 else []
-    co = [nm for b, nm in ((8, "bomb"), (2, "vertical_laser"), (4, "horizontal_laser")) if sm & b]
-    n = 1500 if R == 10 else 300
-    for blocks in (1, 0):
-        env = TileMatchVecEnv(n, R, C, k, 12, cl, co, seed=8, device=DEV, groups=2)
-        ref = orc.OracleBatch(R, C, k, sm, 12, env.rng_words().copy(), threads=16)
-        env.reset()
-        ref.reset()
-        env.stagger_phases(blocks=blocks)
-        ref.timer[:] = env.timer.cpu().numpy()
-        acts = synthetic_actions(range(n), 26, env.num_actions)
-        dacts = torch.from_numpy(acts).to(DEV)
-        for t in range(26):
-            env.step_raw(dacts[t])
-            ref.step(acts[t], autoreset=True)
-            env.join()
-            assert np.array_equal(env.board.cpu().numpy(), ref.board), (blocks, t)
-            assert np.array_equal(env.flags.cpu().numpy(), ref.flags), (blocks, t)
-        assert np.array_equal(env.rng_words(), ref.rng)
-        assert np.array_equal(env.eff.cpu().numpy().view(np.uint64), ref.eff)

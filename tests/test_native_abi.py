@@ -52,6 +52,10 @@ def test_specials_mask_and_spaces():
     assert b.shape == (2, 3, 4) and b.contains(b.sample())
     D = Dict({"board": b, "num_moves_left": d})
     assert D["board"] is b and D.contains(D.sample())
+    from tile_match_gym_amd.spaces import MultiDiscrete
+    m = MultiDiscrete(np.full(7, 180, np.int64), seed=3)            # batched Discrete(180) over 7 envs
+    x = m.sample()
+    assert m.shape == (7,) and m.contains(x) and not m.contains(np.full(7, 180)) and not m.contains(x[:3])
 
 
 def test_action_table_matches_reference_rule():

@@ -116,15 +116,15 @@ def test_spill_path_gpu(R, C, k, sm):
 
 
 @pytest.mark.gpu
-def test_spill_queue_full_is_flagged():
-    """More envs outgrowing the LDS lists in one launch than the spill queue
-    holds (TMG_SPILL_CAP = 4096): the excess steps are flagged FLAG_OVERFLOW
-    (info["overflow"], STATUS_OVERFLOW) instead of passing silently; the
-    queued ones stay exact."""
-    from tile_match_gym_amd import _native
+def test_spill_queue_holds_every_env_of_a_launch():
+    """More envs outgrowing the LDS lists in one launch than round 2's fixed
+    queue held (4096): the per-stream spill queue is sized by the host for the
+    launch (tmg_capi.hip spill_for), so every one of them is re-run on the
+    worst-case lists, bit-exact vs the oracle, and nothing is flagged (the
+    reference's Python lists are unbounded, board.py:149-215, 269-327)."""
     from tile_match_gym_amd.vec_env import TileMatchVecEnv
     R, C, k, sm = 20, 20, 6, 15
-    n = 4096 + 512
+    n = 6144
     b = adversarial_boards(n, R, C, k, sm, 3, "combo_grid")
     a = effective_actions(b)
     env = TileMatchVecEnv(n, R, C, k, 30, ["cookie"], ["vertical_laser", "horizontal_laser", "bomb"], seed=5,
@@ -133,11 +133,13 @@ def test_spill_queue_full_is_flagged():
     env.board.copy_(torch.from_numpy(b))
     o.board[:] = b
     env.invalidate_effective_cache()
+    s0 = env.ctx.spills()
     _, _, _, _, info = env.step(torch.from_numpy(a).to("cuda:0"))
     o.step(a, autoreset=True)
-    ovf = info["overflow"].cpu().numpy()
-    assert ovf.sum() > 0
-    assert env.status() & _native.STATUS_OVERFLOW
-    good = ~ovf
-    assert np.array_equal(env.board.cpu().numpy()[good], o.board[good])
-    assert np.array_equal(env.reward.cpu().numpy()[good], o.reward[good])
+    spilled = env.ctx.spills() - s0
+    assert spilled > 4096, f"only {spilled} envs of the launch outgrew the LDS lists"
+    v = _Vec(env)
+    for f in ("board", "rng", "reward", "n_new", "n_act", "flags", "eff", "timer"):
+        assert np.array_equal(getattr(v, f), getattr(o, f)), f
+    assert not info["overflow"].any() and not info["error"].any()
+    assert env.status() == 0

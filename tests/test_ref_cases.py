@@ -208,3 +208,44 @@ def test_ref_board_facade_gpu():
                 assert is_move_effective(r["board"], c2, c1) == bool(r["eff"][a])
         n += 1
     assert n >= 100
+
+
+@pytest.mark.gpu
+def test_ref_combination_boards_gpu():
+    """The reference's combination_match boards (test_combination_match.py:6-417:
+    every special pair) driven through tmg_step with their recorded action on
+    the kernels — combination, gravity, refill, the cascade and the
+    ensure-playable loop (board.py:357-391, 600-719) — from 16 PCG64 states
+    each, against the oracle's move() on the same inputs."""
+    from tile_match_gym_amd.seeding import batch_rng_words
+    dev = "cuda:0"
+    s = torch.cuda.current_stream().cuda_stream
+    reps, total = 16, 0
+    for (R, C, k, sm), recs in _by_shape(load_records("combo", "ref")).items():
+        ctx = _ctx(R, C, k, sm)
+        assert ctx is not None, (R, C, k)
+        boards = np.stack([r["board"] for r in recs for _ in range(reps)]).astype(np.int8)
+        acts = np.array([int(r["action"]) for r in recs for _ in range(reps)], np.int32)
+        n = boards.shape[0]
+        words = batch_rng_words(range(4000 + total, 4000 + total + n))
+        board = torch.from_numpy(boards).to(dev)
+        rng = torch.from_numpy(words.view(np.int64).copy()).to(dev)
+        timer = torch.zeros(n, dtype=torch.int32, device=dev)
+        dacts = torch.from_numpy(acts).to(dev)
+        out = torch.zeros((3, n), dtype=torch.int32, device=dev)
+        flags = torch.zeros(n, dtype=torch.uint8, device=dev)
+        eff = torch.zeros((n, ctx.mask_words), dtype=torch.int64, device=dev)
+        ctx.step(n, board.data_ptr(), rng.data_ptr(), timer.data_ptr(), dacts.data_ptr(), out[0].data_ptr(),
+                 out[1].data_ptr(), out[2].data_ptr(), flags.data_ptr(), eff.data_ptr(), 0, 0, s)
+        torch.cuda.synchronize()
+        b, rw, o, f = board.cpu().numpy(), rng.cpu().numpy().view(np.uint64), out.cpu().numpy(), flags.cpu().numpy()
+        for i in range(n):
+            want_b, want_rng, res, err = orc.move(boards[i], words[i], int(acts[i]), k, sm)
+            assert err == 0
+            assert res[1] == 1, "a combination record must take the combination branch"
+            assert np.array_equal(b[i], want_b), ((R, C, k, sm), i)
+            assert np.array_equal(rw[i], want_rng), ((R, C, k, sm), i)
+            assert (o[0, i], o[1, i], o[2, i]) == (res[0], res[2], res[3]), ((R, C, k, sm), i)
+            assert bool(f[i] & 2) and bool(f[i] & 4) == bool(res[4]) and not (f[i] & 0xC0)
+        total += n
+    assert total == 13 * reps

@@ -101,26 +101,61 @@ enum : uint32_t { ST_INTERNAL = 1, ST_OVERFLOW = 2, ST_CALLER = 4 };
 #define TMG_MAX_SHUFFLES (1 << 12)   // shuffles per loop
 #endif
 
-// Per-stream queue of the envs whose step ran out of LDS list space (step_env)
-#ifndef TMG_SPILL_CAP
-#define TMG_SPILL_CAP 4096       // queued envs per step launch
-#endif
+// Per-stream queue of the envs whose step ran out of LDS list space
+// (step_env), drained by spill_kernel.  Sized by the host for the envs of
+// the launch (cap >= n), so every such env fits: no step is ever dropped.
 #ifndef TMG_SPILL_WAVES
-#define TMG_SPILL_WAVES 8        // spill_kernel workgroups (one wave, one WsSerialBig each)
+#define TMG_SPILL_WAVES 32       // spill_kernel workgroups (one wave, one WsSerialBig each)
 #endif
 struct SpillQ {
     uint32_t count, done;        // queued envs; spill_kernel waves finished
     unsigned long long total;    // envs re-run so far (diagnostic, tmg_spills)
-    int64_t env[TMG_SPILL_CAP];
+    int64_t cap;                 // entries of env[] (>= the envs of any launch on this stream)
+    int64_t env[1];              // [cap]
 };
 
-// Per-stream queue of the envs a deferred-autoreset step finished (step_env
-// with autoreset == 2), drained by reset_queue_kernel.  Sized by the host for
-// the launch's env count.
-struct ResetQ {
-    uint32_t count, next, done, pad;   // queued envs; next to take; waves finished
-    int64_t env[1];                    // [capacity]
+// Diagnostic build only (TMG_COVER=1, never the product library): per-branch
+// hit counters of the cascade step forms (tmg_debug_cover), so tests can show
+// that every wave-parallel form and the lane-0 fallback ran.
+#ifndef TMG_COVER
+#define TMG_COVER 0
+#endif
+enum : int {
+    CV_SB_LEAN = 0,      // lean bitboard cascade step (no specials enabled)
+    CV_SB_NORMAL,        // sb_simple_step: plain normal matches only
+    CV_SB_LASER,         // sb_simple_step: a laser created
+    CV_SB_PERP_BOMB,     // sb_simple_step: a bomb with a perpendicular (crossing) run
+    CV_SB_ROW_BOMB,      // sb_simple_step: a bomb with a row-rs run (bomb_plan)
+    CV_SB_CLOSURE,       // sb_simple_step: matched specials activated (closure)
+    CV_SB_FALLBACK,      // sb_simple_step declined: lane-0 list step follows
+    CV_LDS_NORMAL,       // simple_step_lds (512-cell kernels): normal matches only
+    CV_LDS_LASER,        // simple_step_lds: a laser created
+    CV_LDS_BOMB,         // simple_step_lds: a bomb (bomb_plan)
+    CV_LDS_FALLBACK,     // simple_step_lds declined on a plain board
+    CV_SERIAL_STEP,      // lane-0 list step (get_colour_lines / process / resolve)
+    CV_SERIAL_ACT,       // activate_special entered on the lane-0 path
+    CV_SERIAL_COOKIE,    // a cookie activated on the lane-0 path
+    CV_COMBO,            // combination_match
+    CV_SPILL,            // step queued for spill_kernel
+    CV_SPILL_RUN,        // step re-run by spill_kernel
+    CV_SHUFFLE,          // shuffle in the ensure-playable loop
+    CV_REJECT,           // Lemire rejection: serial replay of a draw batch
+    CV_FAST,             // fast_clear step (general kernel, no specials enabled)
+    CV_COUNT = 32
 };
+#if TMG_COVER
+#define COVER(site)                                                                                     \
+    do {                                                                                                \
+        if (lane == 0 && P.cover) atomicAdd(P.cover + (site), 1ULL);                                   \
+    } while (0)
+#define COVER_L0(site)                                                                                  \
+    do {                                                                                                \
+        if (P.cover) atomicAdd(P.cover + (site), 1ULL);                                                \
+    } while (0)
+#else
+#define COVER(site) ((void)0)
+#define COVER_L0(site) ((void)0)
+#endif
 
 struct Params {
     int R, C, N, A, W, k, smask, num_moves;
@@ -141,7 +176,8 @@ struct Params {
     uint32_t oh_sel;              // type ids of the special channels, int8 each (wrappers.py:37-46)
     SpillQ *spill;                // this launch's stream's spill queue (general kernels)
     void *spill_ws;               // TMG_SPILL_WAVES WsSerialBig<MAXN> for spill_kernel
-    ResetQ *resetq;               // deferred autoresets go here (null: FL_RESET-masked reset launch)
+    unsigned long long *cover;    // TMG_COVER builds: CV_COUNT hit counters (null otherwise)
+    uint64_t *stamps;             // TMG_STAMPS builds: per-env phase stamps (null otherwise)
 };
 
 // host: the per-row masks of Params::sb_rows (boards of <= 128 cells)
@@ -173,7 +209,8 @@ inline Params make_params(int R, int C, int k, int smask, int num_moves, const u
     P.status = nullptr;
     P.spill = nullptr;
     P.spill_ws = nullptr;
-    P.resetq = nullptr;
+    P.cover = nullptr;
+    P.stamps = nullptr;
     P.oh = nullptr;
     P.oh_dtype = P.oh_ch = P.oh_nsel = 0;
     P.oh_sel = 0;
@@ -206,14 +243,13 @@ __device__ __forceinline__ int div_cm1(const Params &P, int x) { return (int)(((
 #endif
 #if TMG_STAMPS
 constexpr int kStampEnvs = 1 << 18, kStampSlots = 8;
-__device__ uint64_t g_stamps[kStampEnvs * kStampSlots];
 #define STAMP(e, slot)                                                                           \
     do {                                                                                         \
-        if (lane == 0 && (e) < kStampEnvs) g_stamps[(e) * kStampSlots + (slot)] = __builtin_amdgcn_s_memrealtime(); \
+        if (lane == 0 && P.stamps && (e) < kStampEnvs) P.stamps[(e) * kStampSlots + (slot)] = __builtin_amdgcn_s_memrealtime(); \
     } while (0)
 #define STAMPV(e, slot, v)                                                                       \
     do {                                                                                         \
-        if (lane == 0 && (e) < kStampEnvs) g_stamps[(e) * kStampSlots + (slot)] = (uint64_t)(v); \
+        if (lane == 0 && P.stamps && (e) < kStampEnvs) P.stamps[(e) * kStampSlots + (slot)] = (uint64_t)(v); \
     } while (0)
 #else
 #define STAMP(e, slot) ((void)0)
@@ -453,6 +489,7 @@ __device__ __forceinline__ void draw_colours(const Params &P, int lane, const La
         last_hi = rdlane64(out >> 32, cnt - 1);
     }
     if (P.thr != 0u && __ballot(rej) != 0ULL) {            // Lemire rejection: exact serial replay
+        COVER(CV_REJECT);
         WFENCE();
         if (lane == 0) {
             Rng r = g0;
@@ -959,6 +996,7 @@ __device__ __forceinline__ int ensure_playable(const Params &P, WS &w, int lane,
         }
         if (scan_effective(P, w, lane, cl, (P.smask & SP_COOKIE) == 0)) break;
         if (shuffles >= TMG_MAX_SHUFFLES) return fl | FL_ERR;
+        COVER(CV_SHUFFLE);
         WSYNC();
         shuffle(P, w, lane, g);
         fl = FL_SHUF;
@@ -978,12 +1016,13 @@ __device__ __forceinline__ int generate_board(const Params &P, WS &w, int lane, 
     return ensure_playable<ROLL, PRE, true>(P, w, lane, J, g, cl) & FL_ERR;         // types all 1
 }
 
-// Queue env e for spill_kernel; false when the queue is full.
+// Queue env e for spill_kernel.  The host sizes the queue for every env of
+// the launch, so this cannot fail; false only if that sizing were broken.
 __device__ __forceinline__ bool spill_enqueue(const Params &P, int lane, int64_t e) {
     int ok = 0;
     if (lane == 0) {
         const uint32_t i = atomicAdd(&P.spill->count, 1u);
-        if (i < (uint32_t)TMG_SPILL_CAP) { P.spill->env[i] = e; ok = 1; }
+        if ((int64_t)i < P.spill->cap) { P.spill->env[i] = e; ok = 1; }
     }
     return __ballot(ok) != 0ULL;
 }
@@ -1239,6 +1278,9 @@ __device__ __forceinline__ int simple_step_lds(const Params &P, WS &w, int lane,
     }
     if (!ok) { WSYNC(); return 0; }
     if (lane == 0) w.sc[SC_NNEW] += __popcll(hl) + __popcll(vl) + __popcll(bombc);
+    if (hl | vl) COVER(CV_LDS_LASER);
+    if (bombc) COVER(CV_LDS_BOMB);
+    if (!(hl | vl | bombc)) COVER(CV_LDS_NORMAL);
     WSYNC();
     return cleared;
 }
@@ -1457,6 +1499,7 @@ struct Serial {
         if (t == 0 || t == 1) { w.sc[SC_ERR] = 1; return; }  // :491-492
         clr(cell);                                           // :496
         if (!combo) w.sc[SC_NACT]++;                         // :498-499
+        COVER_L0(t == -1 ? CV_SERIAL_COOKIE : CV_SERIAL_ACT);
         if (sp >= LS::MSTK) { ovf = true; return; }
         if (t == 2 || t == 3 || t == 4) {
             s.fcell[sp] = (int16_t)cell; s.ftype[sp] = (int8_t)t; s.fidx[sp] = 0; s.faux[sp] = 0; sp++;
@@ -1681,6 +1724,7 @@ __device__ __forceinline__ int board_move(const Params &P, Ws<MAXN, GEN> &w, int
     bool ovf = false, err = false;
     if (((t1 != 0 && t1 != 1) && (t2 != 0 && t2 != 1)) || t1 < 0 || t2 < 0) {   // :357-364
         flags |= FL_COMBO;
+        COVER(CV_COMBO);
         if constexpr (GEN) {
             int nz = count_colour_nonzero(P, w, lane);
             if (lane == 0) {
@@ -1720,6 +1764,7 @@ __device__ __forceinline__ int board_move(const Params &P, Ws<MAXN, GEN> &w, int
                 const int r = sb_simple_step<SBNB, CODD>(P, w, lane, J, g);
                 if (r < 0) break;
                 if (r > 0) { elim += r; iters++; lim = P.R - 1; continue; }
+                COVER(CV_SB_FALLBACK);
             }
         }
         Det<MAXN / 64> d;
@@ -1727,6 +1772,7 @@ __device__ __forceinline__ int board_move(const Params &P, Ws<MAXN, GEN> &w, int
         if (rs < 0) break;
         lim = P.R - 1;
         if (fast) {
+            COVER(CV_FAST);
             elim += fast_clear(P, w, lane, cl, d, rs);      // clears rows <= rs only (a deeper run would be a lower line)
             lim = min(P.R - 1, rs + 2);
         } else {
@@ -1743,9 +1789,11 @@ __device__ __forceinline__ int board_move(const Params &P, Ws<MAXN, GEN> &w, int
                     lim = min(P.R - 1, rs + 2);
                     continue;
                 }
+                if (plain) COVER(CV_LDS_FALLBACK);
             }
             if constexpr (GEN) {
                 int nz = count_colour_nonzero(P, w, lane);
+                COVER(CV_SERIAL_STEP);
                 if (lane == 0) {
                     w.sc[SC_NZ] = nz;
                     Serial<MAXN, L> S(P, w, *lists);
@@ -1821,6 +1869,11 @@ __device__ __forceinline__ uint32_t step_env(
     const int t0 = __builtin_amdgcn_readfirstlane(timer[e]);
     if (t0 >= P.num_moves || a < 0 || a >= P.A) {                           // tile_match_env.py:94-95
         if (lane == 0) { reward[e] = 0; n_new[e] = 0; n_act[e] = 0; flags_out[e] = FL_ERR; }
+        if (P.oh && !trust_eff) {             // the fused planes follow every board of an untrusted call
+            load_board(P, w, lane, board + e * 2 * N);
+            WSYNC();
+            store_onehot(P, w, lane, e);
+        }
         return ST_CALLER;
     }
     int8_t *gb = board + e * 2 * N;
@@ -1836,7 +1889,6 @@ __device__ __forceinline__ uint32_t step_env(
         if (lane == 0) {
             timer[e] = defer ? 0 : t1; reward[e] = 0; n_new[e] = 0; n_act[e] = 0;
             flags_out[e] = (uint8_t)(flags | (defer ? FL_RESET : 0));
-            if (defer && P.resetq) P.resetq->env[atomicAdd(&P.resetq->count, 1u)] = e;
         }
         STAMP(e, 7);
         return 0;
@@ -1872,11 +1924,19 @@ __device__ __forceinline__ uint32_t step_env(
         if constexpr (SBNB > 0 && !GEN) elim = sb_move<SBNB, CODD>(P, w, lane, J, g, cl, p1, p2, flags, e);
         else elim = board_move<MAXN, GEN, SBNB, CODD, L>(P, w, lane, J, g, cl, p1, p2, flags, nn, na, e, lists, trust_eff != 0);
         changed = true;
-        if constexpr (GEN && !SPILL) {
-            // the LDS lists ran out: nothing of this env has been written; queue
-            // it for spill_kernel, which re-runs the whole step on lists sized
-            // for the worst case (a full queue leaves the step flagged FL_OVF)
-            if ((flags & FL_OVF) && spill_enqueue(P, lane, e)) return 0;
+        if constexpr (GEN) {
+            if (flags & FL_OVF) {
+                // the LDS lists ran out: nothing of this env has been written;
+                // queue it for spill_kernel, which re-runs the whole step on
+                // lists sized for the worst case (WsSerialBig).  The queue holds
+                // every env of the launch and WsSerialBig cannot run out, so the
+                // fall-through is unreachable; were it reached, the step is
+                // flagged as an internal error, never written back as exact.
+                if constexpr (!SPILL) {
+                    if (spill_enqueue(P, lane, e)) { COVER(CV_SPILL); return 0; }
+                }
+                flags = (flags & ~FL_OVF) | FL_ERR;
+            }
         }
     }
     STAMP(e, 4);
@@ -1891,7 +1951,6 @@ __device__ __forceinline__ uint32_t step_env(
         }                                      // autoreset == 2: reset_kernel regenerates FL_RESET envs next
         tnew = 0;
         flags |= FL_RESET;
-        if (autoreset == 2 && lane == 0 && P.resetq) P.resetq->env[atomicAdd(&P.resetq->count, 1u)] = e;
     }
     STAMP(e, 5);
     if (changed) {
@@ -1960,12 +2019,14 @@ __global__ __launch_bounds__(64) void spill_kernel(
     WS &w = *reinterpret_cast<WS *>(smem);
     SpillQ *q = P.spill;
     WsSerialBig<MAXN> *lists = reinterpret_cast<WsSerialBig<MAXN> *>(P.spill_ws) + blockIdx.x;
-    const int cnt = min(__builtin_amdgcn_readfirstlane((int)q->count), TMG_SPILL_CAP);
+    const int64_t queued = (int64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)q->count);
+    const int cnt = (int)(queued < q->cap ? queued : q->cap);
     int done = 0;
     for (int i = (int)blockIdx.x; i < cnt; i += (int)gridDim.x) {
         const int64_t e = (int64_t)bcast64((uint64_t)q->env[i]);
         if (e < 0 || e >= n) continue;
         WSYNC();
+        COVER(CV_SPILL_RUN);
         const uint32_t st = step_env<MAXN, true, 0, false, true, WsSerialBig<MAXN>>(
             P, w, lane, e, board, rng, timer, actions, reward, n_new, n_act, flags_out, eff, trust_eff, autoreset, lists);
         note_status(P, lane, st);
@@ -2012,34 +2073,6 @@ __global__ __launch_bounds__(64 * TMG_WPB, MAXN > 128 ? TMG_RESET512_WAVES : 1) 
     if (e >= n) return;
     if (env_mask && !(__builtin_amdgcn_readfirstlane((int)env_mask[e]) & mask_bits)) return;
     reset_env<MAXN, SBNB, CODD>(P, w, lane, e, board, rng, timer, eff);
-}
-
-// The deferred autoresets of one step launch: the envs its step kernel queued
-// (P.resetq), drained by a fixed grid of one-wave workgroups.  Workgroup b
-// takes entry b first, then, while entries remain, the next untaken one
-// (q->next, counting from the grid size): no atomic at all when the queue
-// holds at most one entry per workgroup (a step where few episodes end), and
-// the long regenerations of a storm spread over the grid as waves free up.
-// Every lane takes part in the fetch (lane 0 adds 1, the others 0), so the
-// loop exit stays wave-uniform.  The host zeroes the queue after the launch.
-template <int MAXN, int SBNB = 0, bool CODD = false>
-__global__ __launch_bounds__(64, MAXN > 128 ? TMG_RESET512_WAVES : TMG_RQ128_WAVES) void reset_queue_kernel(
-    Params P, int8_t *__restrict__ board, uint64_t *__restrict__ rng, int32_t *__restrict__ timer,
-    uint64_t *__restrict__ eff) {
-    TMG_SMEM_DECL(smem);
-    using WS = Ws<MAXN, false>;
-    const int lane = threadIdx.x & 63;
-    WS &w = *reinterpret_cast<WS *>(smem);
-    ResetQ *q = P.resetq;
-    const uint32_t cnt = (uint32_t)__builtin_amdgcn_readfirstlane((int)q->count);
-    uint32_t i = blockIdx.x;
-    while (i < cnt) {
-        const int64_t e = (int64_t)bcast64((uint64_t)q->env[i]);
-        WSYNC();
-        reset_env<MAXN, SBNB, CODD>(P, w, lane, e, board, rng, timer, eff);
-        if (cnt <= gridDim.x) break;
-        i = gridDim.x + (uint32_t)__builtin_amdgcn_readfirstlane((int)atomicAdd(&q->next, lane == 0 ? 1u : 0u));
-    }
 }
 
 // TileMatchEnv._get_effective_actions for arbitrary boards (tile_match_env.py:118-124)

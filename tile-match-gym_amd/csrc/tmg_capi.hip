@@ -1,16 +1,26 @@
 // tmg_capi.hip — extern "C" entry points of libtmg.so (declared in include/tmg.h).
+// Host code only: the kernels and their launchers live in tmg_kernels.hip
+// (one translation unit per kernel group, tmg_launch.h).
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <mutex>
 #include <string>
 #include <utility>
 #include <vector>
 
 #include "tmg.h"
 #include "tmg_board.hip"
-#include "tmg_aux.hip"
+#include "tmg_launch.h"
+
+#ifndef TMG_SRC_SHA
+#define TMG_SRC_SHA "unknown"
+#endif
+#ifndef TMG_VARIANT
+#define TMG_VARIANT "product"
+#endif
 
 namespace {
 
@@ -34,143 +44,79 @@ struct tmg_ctx {
     uint64_t *d_jump;
     uint64_t *d_sbrows;
     uint32_t *d_status;  // sticky status words (tmg_status): one per TMG_STATUS_* bit
+    unsigned long long *d_cover;   // TMG_COVER builds only
+    uint64_t *d_stamps;            // TMG_STAMPS builds only
     int maxn;
-    int sb;          // scalar-bitboard kernels usable (<= 128 cells, C <= 63); TMG_SB=0 disables (A/B)
-    int defer_general;   // 128-cell general kernel: autoreset by a masked reset launch (TMG_DEFER=0 disables)
-    // spill queues of the general kernels, one per stream the context steps on
-    // (a queue is only ever touched by the launches of its own stream, in order)
+    int sb;              // scalar-bitboard kernels (<= 128 cells, C <= 63)
+    int scan_only;       // tmg_create_scan: tmg_effective / tmg_onehot only
+    // spill queue of the general kernels, one per stream the context steps on
+    // (a queue is only ever touched by the launches of its own stream, in
+    // order), holding at least as many entries as the largest launch on it
     struct Spill {
         hipStream_t stream;
         tmg::SpillQ *q;
+        int64_t cap;
         void *ws;
-        tmg::ResetQ *rq;     // deferred-autoreset queue of this stream
-        int64_t rq_cap;
     };
     std::vector<Spill> spills;
-    int spill_launch;    // TMG_SPILL=0 skips the spill launches (cost A/B only: overflowing steps are then lost)
-    int reset_queue;     // deferred autoresets through a queue (TMG_RESETQ=1) instead of an FL_RESET-masked launch
+    std::mutex mu;       // guards `spills` (calls on different streams may come from several threads)
 };
 
 using tmg::Params;
+using tmg::StepArgs;
 
-struct StepArgs {
-    int64_t n;
-    int8_t *board;
-    uint64_t *rng;
-    int32_t *timer;
-    const int32_t *actions;
-    int32_t *reward, *n_new, *n_act;
-    uint8_t *flags;
-    uint64_t *eff;
-    int trust_eff, autoreset;
-};
-
-template <int MAXN, bool GEN, int NB, bool CODD>
-static void launch_step(dim3 grid, hipStream_t s, const Params &P, const StepArgs &a) {
-    const size_t lds = sizeof(tmg::Ws<MAXN, GEN>) * TMG_WPB;
-    hipLaunchKernelGGL((tmg::step_kernel<MAXN, GEN, NB, CODD>), grid, dim3(64 * TMG_WPB), lds, s, P, a.n, a.board,
-                       a.rng, a.timer, a.actions, a.reward, a.n_new, a.n_act, a.flags, a.eff, a.trust_eff, a.autoreset);
-}
-
-// the stream's spill queue (allocated zeroed on first use)
-static int spill_for(tmg_ctx *ctx, hipStream_t s, tmg::SpillQ **q, void **ws) {
-    for (const auto &x : ctx->spills)
-        if (x.stream == s) { *q = x.q; *ws = x.ws; return 0; }
-    const size_t wsz = ctx->maxn == 128 ? sizeof(tmg::WsSerialBig<128>) : sizeof(tmg::WsSerialBig<512>);
-    tmg_ctx::Spill sp{s, nullptr, nullptr, nullptr, 0};
-    int rc = hip_check(hipMalloc(&sp.q, sizeof(tmg::SpillQ)), "hipMalloc");
-    if (!rc) rc = hip_check(hipMalloc(&sp.ws, wsz * TMG_SPILL_WAVES), "hipMalloc");
-    // zeroed in order on s itself (a memset on the null stream is not ordered
-    // with respect to a non-blocking stream's launches)
-    if (!rc) rc = hip_check(hipMemsetAsync(sp.q, 0, sizeof(tmg::SpillQ), s), "hipMemsetAsync");
-    if (rc) {
-        if (sp.q) (void)hipFree(sp.q);
-        if (sp.ws) (void)hipFree(sp.ws);
-        return rc;
-    }
-    ctx->spills.push_back(sp);
-    *q = sp.q;
-    *ws = sp.ws;
-    return 0;
-}
-
-// the stream's deferred-autoreset queue, holding at least n envs (zeroed on s)
-static int resetq_for(tmg_ctx *ctx, hipStream_t s, int64_t n, tmg::ResetQ **out) {
-    tmg_ctx::Spill *sp = nullptr;
-    for (auto &x : ctx->spills)
-        if (x.stream == s) sp = &x;
-    if (!sp) return fail(-5, "no spill entry for this stream");
-    if (sp->rq_cap < n) {
-        int rc = 0;
-        if (sp->rq) {                                  // grow: the old queue may still be in use on s
-            rc = hip_check(hipStreamSynchronize(s), "hipStreamSynchronize");
-            (void)hipFree(sp->rq);
-            sp->rq = nullptr;
-            sp->rq_cap = 0;
-        }
-        const size_t bytes = sizeof(tmg::ResetQ) + (size_t)n * sizeof(int64_t);
-        if (!rc) rc = hip_check(hipMalloc(&sp->rq, bytes), "hipMalloc");
-        if (!rc) rc = hip_check(hipMemsetAsync(sp->rq, 0, sizeof(tmg::ResetQ), s), "hipMemsetAsync");
-        if (rc) return rc;
-        sp->rq_cap = n;
-    }
-    *out = sp->rq;
-    return 0;
-}
-
-template <int MAXN, int NB, bool CODD>
-static void launch_reset_queue(hipStream_t s, const Params &P, int64_t n, int8_t *board, uint64_t *rng,
-                               int32_t *timer, uint64_t *eff) {
-    // a fixed grid of one-wave workgroups draining the queue: about the waves
-    // the chip holds at the kernel's occupancy (the queue holds <= n envs)
-    const int64_t full = MAXN > 128 ? 256 * 4 * TMG_RESET512_WAVES : 256 * 4 * TMG_RQ128_WAVES;
-    const unsigned g = (unsigned)(n < full ? n : full);
-    hipLaunchKernelGGL((tmg::reset_queue_kernel<MAXN, NB, CODD>), dim3(g), dim3(64), sizeof(tmg::Ws<MAXN, false>), s,
-                       P, board, rng, timer, eff);
-    (void)hipMemsetAsync(P.resetq, 0, 16, s);                // count / next / done for the next launch
-}
-
-template <int MAXN>
-static void launch_spill(hipStream_t s, const Params &P, const StepArgs &a) {
-    const size_t lds = sizeof(tmg::Ws<MAXN, true>);
-    hipLaunchKernelGGL((tmg::spill_kernel<MAXN>), dim3(TMG_SPILL_WAVES), dim3(64), lds, s, P, a.n, a.board, a.rng,
-                       a.timer, a.actions, a.reward, a.n_new, a.n_act, a.flags, a.eff, a.trust_eff, a.autoreset);
-}
-
-template <int MAXN, int NB, bool CODD>
-static void launch_reset(dim3 grid, hipStream_t s, const Params &P, int64_t n, int8_t *board, uint64_t *rng,
-                         int32_t *timer, uint64_t *eff, const uint8_t *env_mask, int mask_bits) {
-    const size_t lds = sizeof(tmg::Ws<MAXN, false>) * TMG_WPB;
-    hipLaunchKernelGGL((tmg::reset_kernel<MAXN, NB, CODD>), grid, dim3(64 * TMG_WPB), lds, s, P, n, board, rng, timer,
-                       eff, env_mask, mask_bits);
-}
-
-// scalar-bitboard variants: NB colour planes, C odd or even
-template <bool GEN, bool CODD>
-static void launch_step_sb(dim3 grid, hipStream_t s, const Params &P, const StepArgs &a) {
-    switch (tmg::sb_planes(P.k)) {
-    case 1: launch_step<128, GEN, 1, CODD>(grid, s, P, a); break;
-    case 2: launch_step<128, GEN, 2, CODD>(grid, s, P, a); break;
-    case 3: launch_step<128, GEN, 3, CODD>(grid, s, P, a); break;
-    default: launch_step<128, GEN, 4, CODD>(grid, s, P, a); break;
-    }
-}
-template <bool CODD>
-static void launch_reset_sb(dim3 grid, hipStream_t s, const Params &P, int64_t n, int8_t *board, uint64_t *rng,
-                            int32_t *timer, uint64_t *eff, const uint8_t *env_mask, int mask_bits) {
-    switch (tmg::sb_planes(P.k)) {
-    case 1: launch_reset<128, 1, CODD>(grid, s, P, n, board, rng, timer, eff, env_mask, mask_bits); break;
-    case 2: launch_reset<128, 2, CODD>(grid, s, P, n, board, rng, timer, eff, env_mask, mask_bits); break;
-    case 3: launch_reset<128, 3, CODD>(grid, s, P, n, board, rng, timer, eff, env_mask, mask_bits); break;
-    default: launch_reset<128, 4, CODD>(grid, s, P, n, board, rng, timer, eff, env_mask, mask_bits); break;
-    }
-}
-
-// one wave per env: grid padded to 8 equal XCD blocks (wg_env0)
-static dim3 env_grid(int64_t n) {
+namespace tmg {
+dim3 env_grid(int64_t n) {
     int64_t nwg = (n + TMG_WPB - 1) / TMG_WPB;
     if (TMG_XCD) nwg = (nwg + 7) & ~(int64_t)7;
     return dim3((unsigned)nwg);
+}
+size_t spill_ws_bytes(int maxn) {
+    return maxn <= 128 ? sizeof(WsSerialBig<128>) : sizeof(WsSerialBig<512>);
+}
+}  // namespace tmg
+
+// The stream's spill queue, holding at least n entries (zeroed on s).  Growing
+// waits for s first: the old queue may still be read by a queued launch.
+static int spill_for(tmg_ctx *ctx, hipStream_t s, int64_t n, tmg::SpillQ **q, void **ws) {
+    std::lock_guard<std::mutex> lock(ctx->mu);
+    tmg_ctx::Spill *sp = nullptr;
+    for (auto &x : ctx->spills)
+        if (x.stream == s) sp = &x;
+    if (!sp) {
+        ctx->spills.push_back(tmg_ctx::Spill{s, nullptr, 0, nullptr});
+        sp = &ctx->spills.back();
+        int rc = hip_check(hipMalloc(&sp->ws, tmg::spill_ws_bytes(ctx->maxn) * TMG_SPILL_WAVES), "hipMalloc");
+        if (rc) { ctx->spills.pop_back(); return rc; }
+    }
+    if (sp->cap < n) {
+        int rc = 0;
+        unsigned long long total = 0;
+        if (sp->q) {
+            rc = hip_check(hipStreamSynchronize(s), "hipStreamSynchronize");
+            if (!rc) rc = hip_check(hipMemcpy(&total, &sp->q->total, sizeof total, hipMemcpyDeviceToHost), "hipMemcpy");
+            (void)hipFree(sp->q);
+            sp->q = nullptr;
+            sp->cap = 0;
+        }
+        const int64_t cap = n < 64 ? 64 : n;
+        const size_t bytes = sizeof(tmg::SpillQ) + (size_t)cap * sizeof(int64_t);
+        if (!rc) rc = hip_check(hipMalloc(&sp->q, bytes), "hipMalloc");
+        if (rc) return rc;
+        tmg::SpillQ h{};
+        h.total = total;
+        h.cap = cap;
+        // written in order on s itself (a copy on the null stream is not
+        // ordered with respect to a non-blocking stream's launches)
+        rc = hip_check(hipMemcpyAsync(sp->q, &h, offsetof(tmg::SpillQ, env), hipMemcpyHostToDevice, s),
+                       "hipMemcpyAsync");
+        if (!rc) rc = hip_check(hipStreamSynchronize(s), "hipStreamSynchronize");   // h leaves scope
+        if (rc) return rc;
+        sp->cap = cap;
+    }
+    *q = sp->q;
+    *ws = sp->ws;
+    return 0;
 }
 
 static int set_device(tmg_ctx *ctx) {
@@ -182,98 +128,55 @@ static int set_device(tmg_ctx *ctx) {
 
 static int do_reset(tmg_ctx *ctx, const Params &P, int64_t n, int8_t *board, uint64_t *rng, int32_t *timer,
                     uint64_t *eff, const uint8_t *env_mask, int mask_bits, hipStream_t s) {
-    const dim3 grid = env_grid(n);
-    if (ctx->maxn == 128) {
-        if (ctx->sb) {
-            if (P.C & 1) launch_reset_sb<true>(grid, s, P, n, board, rng, timer, eff, env_mask, mask_bits);
-            else launch_reset_sb<false>(grid, s, P, n, board, rng, timer, eff, env_mask, mask_bits);
-        } else {
-            launch_reset<128, 0, false>(grid, s, P, n, board, rng, timer, eff, env_mask, mask_bits);
-        }
-    } else {
-        launch_reset<512, 0, false>(grid, s, P, n, board, rng, timer, eff, env_mask, mask_bits);
-    }
+    const dim3 grid = tmg::env_grid(n);
+    if (ctx->maxn == 128) tmg::launch_reset128(ctx->sb, grid, s, P, n, board, rng, timer, eff, env_mask, mask_bits);
+    else tmg::launch_reset512(grid, s, P, n, board, rng, timer, eff, env_mask, mask_bits);
     return hip_check(hipGetLastError(), "kernel launch");
 }
 
 static int do_step(tmg_ctx *ctx, Params P, StepArgs a, hipStream_t s) {
+    // lean kernels: no special can exist (none enabled) and the cached mask
+    // came from this library's own step / reset of the current boards
     const bool lean = ctx->P.smask == 0 && a.trust_eff;
-    const dim3 grid = env_grid(a.n);
+    const dim3 grid = tmg::env_grid(a.n);
     a.autoreset = a.autoreset ? 1 : 0;
-    const int deferred = a.autoreset && (ctx->maxn == 512 || (ctx->defer_general && !lean) || (TMG_LEAN_DEFER && lean));
-    if (!lean || deferred) {                       // this stream's spill / deferred-reset queues
-        int rc = spill_for(ctx, s, &P.spill, &P.spill_ws);
-        if (!rc && deferred && ctx->reset_queue) rc = resetq_for(ctx, s, a.n, &P.resetq);
+    // the general and 512-cell kernels leave finished boards to a reset launch
+    // masked by FL_RESET, which runs at several times their occupancy
+    const int deferred = a.autoreset && (ctx->maxn == 512 || !lean || TMG_LEAN_DEFER);
+    if (!lean) {
+        int rc = spill_for(ctx, s, a.n, &P.spill, &P.spill_ws);
         if (rc) return rc;
     }
-    // 512-cell kernels (and, with defer_general, the 128-cell general one):
-    // finished boards are regenerated by a reset_kernel launch masked by
-    // FL_RESET, which runs at several times the step kernel's occupancy
     if (deferred) a.autoreset = 2;
     if (ctx->maxn == 128) {
-        if (ctx->sb) {
-            if (lean) {
-                if (P.C & 1) launch_step_sb<false, true>(grid, s, P, a);
-                else launch_step_sb<false, false>(grid, s, P, a);
-            } else {
-                if (P.C & 1) launch_step_sb<true, true>(grid, s, P, a);
-                else launch_step_sb<true, false>(grid, s, P, a);
-            }
-        } else if (lean) {
-            launch_step<128, false, 0, false>(grid, s, P, a);
-        } else {
-            launch_step<128, true, 0, false>(grid, s, P, a);
-        }
-    } else if (lean) {
-        launch_step<512, false, 0, false>(grid, s, P, a);
+        if (lean) tmg::launch_step_lean128(ctx->sb, grid, s, P, a);
+        else if (ctx->sb && (P.C & 1)) tmg::launch_step_gen128_odd(grid, s, P, a);
+        else tmg::launch_step_gen128_even(ctx->sb, grid, s, P, a);
     } else {
-        launch_step<512, true, 0, false>(grid, s, P, a);
+        tmg::launch_step512(!lean, grid, s, P, a);
     }
     int rc = hip_check(hipGetLastError(), "kernel launch");
     if (rc) return rc;
-    if (!lean && ctx->spill_launch) {              // re-run the steps that ran out of LDS list space
-        if (ctx->maxn == 128) launch_spill<128>(s, P, a);
-        else launch_spill<512>(s, P, a);
+    if (!lean) {                                   // re-run the steps that ran out of LDS list space
+        if (ctx->maxn == 128) tmg::launch_spill128(s, P, a);
+        else tmg::launch_spill512(s, P, a);
         rc = hip_check(hipGetLastError(), "kernel launch");
         if (rc) return rc;
     }
     if (!deferred) return 0;
-    if (!P.resetq) return do_reset(ctx, P, a.n, a.board, a.rng, a.timer, a.eff, a.flags, tmg::FL_RESET, s);
-    if (ctx->maxn == 512) {
-        launch_reset_queue<512, 0, false>(s, P, a.n, a.board, a.rng, a.timer, a.eff);
-    } else if (ctx->sb) {
-        const bool codd = P.C & 1;
-        switch (tmg::sb_planes(P.k)) {
-        case 1: codd ? launch_reset_queue<128, 1, true>(s, P, a.n, a.board, a.rng, a.timer, a.eff)
-                     : launch_reset_queue<128, 1, false>(s, P, a.n, a.board, a.rng, a.timer, a.eff); break;
-        case 2: codd ? launch_reset_queue<128, 2, true>(s, P, a.n, a.board, a.rng, a.timer, a.eff)
-                     : launch_reset_queue<128, 2, false>(s, P, a.n, a.board, a.rng, a.timer, a.eff); break;
-        case 3: codd ? launch_reset_queue<128, 3, true>(s, P, a.n, a.board, a.rng, a.timer, a.eff)
-                     : launch_reset_queue<128, 3, false>(s, P, a.n, a.board, a.rng, a.timer, a.eff); break;
-        default: codd ? launch_reset_queue<128, 4, true>(s, P, a.n, a.board, a.rng, a.timer, a.eff)
-                      : launch_reset_queue<128, 4, false>(s, P, a.n, a.board, a.rng, a.timer, a.eff); break;
-        }
-    } else {
-        launch_reset_queue<128, 0, false>(s, P, a.n, a.board, a.rng, a.timer, a.eff);
-    }
-    return hip_check(hipGetLastError(), "kernel launch");
-}
-
-static int do_effective(tmg_ctx *ctx, int64_t n, const int8_t *board, uint64_t *eff, hipStream_t s) {
-    const dim3 grid = env_grid(n), block(64 * TMG_WPB);
-    if (ctx->maxn == 128)
-        hipLaunchKernelGGL(tmg::effective_kernel<128>, grid, block, sizeof(tmg::Ws<128, false>) * TMG_WPB, s, ctx->P,
-                           n, board, eff);
-    else
-        hipLaunchKernelGGL(tmg::effective_kernel<512>, grid, block, sizeof(tmg::Ws<512, false>) * TMG_WPB, s, ctx->P,
-                           n, board, eff);
-    return hip_check(hipGetLastError(), "kernel launch");
+    return do_reset(ctx, P, a.n, a.board, a.rng, a.timer, a.eff, a.flags, tmg::FL_RESET, s);
 }
 
 static int check_call(tmg_ctx *ctx, int64_t n) {
     if (!ctx) return fail(-1, "null context");
     if (n < 0) return fail(-2, "negative batch size");
     return set_device(ctx);
+}
+
+static int check_full(tmg_ctx *ctx, int64_t n) {
+    int rc = check_call(ctx, n);
+    if (!rc && ctx->scan_only) return fail(-2, "context made by tmg_create_scan: effective / onehot only");
+    return rc;
 }
 
 // ---------------------------------------------------------------- viability
@@ -311,8 +214,12 @@ bool playable(int *b, int R, int C) {                 // possible_move on a line
 }
 
 // Whether some R x C board with colours < k is line-free and playable:
-// exhaustively when there are at most 2^21 colourings, else by building
-// random line-free boards (row-major, a colour that completes no triple).
+// exhaustively when there are at most 2^21 colourings, else by a randomised
+// depth-first search over line-free row-major fillings (a cell takes a colour
+// that completes no triple with the two cells left of / above it; a dead end
+// backtracks instead of restarting, so 2-colour boards, where a cell can have
+// both colours forbidden, are found too), testing each complete filling for a
+// playable swap.
 bool shape_viable(int R, int C, int k) {
     if (k < 2 || (R < 3 && C < 3)) return false;
     const int N = R * C;
@@ -329,22 +236,105 @@ bool shape_viable(int R, int C, int k) {
     }
     uint64_t x = 0x9E3779B97F4A7C15ULL;
     auto rnd = [&x]() { x ^= x << 13; x ^= x >> 7; x ^= x << 17; return x; };
-    for (int attempt = 0; attempt < 4096; attempt++) {
-        bool ok = true;
-        for (int p = 0; p < N && ok; p++) {
+    const int kk = k < 16 ? k : 16;
+    std::vector<int> order(N * 16), next(N, 0);       // per cell: a random colour order, the next one to try
+    long budget = 1L << 22;                            // cell assignments over the whole search
+    int complete = 0;
+    for (int restart = 0; restart < 64 && budget > 0; restart++) {
+        int p = 0;
+        next[0] = 0;
+        for (int v = 0; v < kk; v++) order[v] = v;
+        for (int v = kk - 1; v > 0; v--) std::swap(order[v], order[rnd() % (v + 1)]);
+        while (p >= 0 && budget-- > 0) {
+            if (p == N) {
+                if (playable(b.data(), R, C)) return true;
+                if (++complete > 4096) return false;   // many line-free boards, none playable
+                p--;
+                continue;
+            }
             const int r = p / C, c = p - r * C;
-            int choices[16], nc = 0;
-            for (int v = 0; v < k && v < 16; v++) {
+            bool placed = false;
+            while (next[p] < kk) {
+                const int v = order[p * 16 + next[p]++];
                 if (c >= 2 && b[p - 1] == v && b[p - 2] == v) continue;
                 if (r >= 2 && b[p - C] == v && b[p - 2 * C] == v) continue;
-                choices[nc++] = v;
+                b[p] = v;
+                placed = true;
+                break;
             }
-            if (nc == 0) ok = false;
-            else b[p] = choices[rnd() % nc];
+            if (!placed) { p--; continue; }              // dead end: backtrack
+            if (++p < N) {
+                next[p] = 0;
+                for (int v = 0; v < kk; v++) order[p * 16 + v] = v;
+                for (int v = kk - 1; v > 0; v--) std::swap(order[p * 16 + v], order[p * 16 + rnd() % (v + 1)]);
+            }
         }
-        if (ok && playable(b.data(), R, C)) return true;
     }
     return false;
+}
+
+int alloc_tables(tmg_ctx *c) {
+    Params &P = c->P;
+    uint64_t tab[64 * 4];
+    tmg::build_jump_table(tab);
+    int rc = hip_check(hipMalloc(&c->d_jump, sizeof tab), "hipMalloc");
+    if (!rc) rc = hip_check(hipMemcpy(c->d_jump, tab, sizeof tab, hipMemcpyHostToDevice), "hipMemcpy");
+    if (!rc) rc = hip_check(hipMalloc(&c->d_status, 16), "hipMalloc");
+    if (!rc) rc = hip_check(hipMemset(c->d_status, 0, 16), "hipMemset");
+    if (!rc && P.N <= 128) {
+        uint64_t rows[64 * 4];
+        tmg::build_sb_rows(P.R, P.C, rows);
+        rc = hip_check(hipMalloc(&c->d_sbrows, sizeof rows), "hipMalloc");
+        if (!rc) rc = hip_check(hipMemcpy(c->d_sbrows, rows, sizeof rows, hipMemcpyHostToDevice), "hipMemcpy");
+    }
+#if TMG_COVER
+    if (!rc) rc = hip_check(hipMalloc(&c->d_cover, tmg::CV_COUNT * sizeof(unsigned long long)), "hipMalloc");
+    if (!rc) rc = hip_check(hipMemset(c->d_cover, 0, tmg::CV_COUNT * sizeof(unsigned long long)), "hipMemset");
+#endif
+#if TMG_STAMPS
+    if (!rc) rc = hip_check(hipMalloc(&c->d_stamps, (size_t)tmg::kStampEnvs * tmg::kStampSlots * 8), "hipMalloc");
+    if (!rc) rc = hip_check(hipMemset(c->d_stamps, 0, (size_t)tmg::kStampEnvs * tmg::kStampSlots * 8), "hipMemset");
+#endif
+    if (!rc) rc = hip_check(hipDeviceSynchronize(), "hipDeviceSynchronize");
+    P.jump = c->d_jump;
+    P.status = c->d_status;
+    P.sb_rows = c->d_sbrows;
+    P.cover = c->d_cover;
+    P.stamps = c->d_stamps;
+    return rc;
+}
+
+void free_ctx(tmg_ctx *c) {
+    if (c->d_jump) (void)hipFree(c->d_jump);
+    if (c->d_status) (void)hipFree(c->d_status);
+    if (c->d_sbrows) (void)hipFree(c->d_sbrows);
+    if (c->d_cover) (void)hipFree(c->d_cover);
+    if (c->d_stamps) (void)hipFree(c->d_stamps);
+    for (const auto &x : c->spills) {
+        if (x.q) (void)hipFree(x.q);
+        if (x.ws) (void)hipFree(x.ws);
+    }
+    delete c;
+}
+
+int new_ctx(tmg_ctx **out, int device, int rows, int cols, int colours, uint32_t specials_mask, int num_moves,
+            int scan_only) {
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return fail(-3, "no HIP device available");
+    if (device < 0 || device >= ndev) return fail(-3, "bad device index");
+    int rc = hip_check(hipSetDevice(device), "hipSetDevice");
+    if (rc) return rc;
+    tmg_ctx *c = new tmg_ctx();
+    c->device = device;
+    c->d_jump = nullptr; c->d_sbrows = nullptr; c->d_status = nullptr; c->d_cover = nullptr; c->d_stamps = nullptr;
+    c->P = tmg::make_params(rows, cols, colours, (int)specials_mask, num_moves, nullptr);
+    c->maxn = c->P.N <= 128 ? 128 : 512;
+    c->sb = c->P.N <= 128 && c->P.C <= 63;
+    c->scan_only = scan_only;
+    rc = alloc_tables(c);
+    if (rc) { free_ctx(c); return rc; }
+    *out = c;
+    return 0;
 }
 
 }  // namespace
@@ -362,77 +352,21 @@ int tmg_create(tmg_ctx **out, int device, int rows, int cols, int colours, uint3
     if (!shape_viable(rows, cols, colours))
         return fail(-2, "no playable board exists for this shape and colour count (the reference's "
                         "generate_board would loop forever, board.py:102-109)");
-    int ndev = 0;
-    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return fail(-3, "no HIP device available");
-    if (device < 0 || device >= ndev) return fail(-3, "bad device index");
-    int rc = hip_check(hipSetDevice(device), "hipSetDevice");
-    if (rc) return rc;
-    tmg_ctx *c = new tmg_ctx();
-    c->device = device;
-    c->P = tmg::make_params(rows, cols, colours, (int)specials_mask, num_moves, nullptr);
-    Params &P = c->P;
-    c->maxn = P.N <= 128 ? 128 : 512;
-    const char *denv = getenv("TMG_DEFER");
-    const char *sbenv = getenv("TMG_SB");
-    c->sb = P.N <= 128 && P.C <= 63 && !(sbenv && sbenv[0] == '0');
-    c->defer_general = c->sb && !(denv && denv[0] == '0');
-    const char *spenv = getenv("TMG_SPILL");
-    c->spill_launch = !(spenv && spenv[0] == '0');
-    // TMG_RESETQ=1: deferred autoresets through the per-stream queue instead of
-    // the FL_RESET-masked launch.  Measured on c3: -54 us per normal step (no
-    // wave per env to dispatch) but +2.1 ms per reset storm (the looping queue
-    // kernel needs 87 VGPRs, 5 waves/SIMD, against the reset kernel's 69 / 7):
-    // -5 % overall, so off by default.
-    const char *rqenv = getenv("TMG_RESETQ");
-    c->reset_queue = rqenv && rqenv[0] == '1';
-    uint64_t tab[64 * 4];
-    tmg::build_jump_table(tab);
-    rc = hip_check(hipMalloc(&c->d_jump, sizeof tab), "hipMalloc");
-    if (rc) { delete c; return rc; }
-    rc = hip_check(hipMemcpy(c->d_jump, tab, sizeof tab, hipMemcpyHostToDevice), "hipMemcpy");
-    if (rc) { (void)hipFree(c->d_jump); delete c; return rc; }
-    P.jump = c->d_jump;
-    c->d_sbrows = nullptr;
-    c->d_status = nullptr;
-    rc = hip_check(hipMalloc(&c->d_status, 16), "hipMalloc");
-    if (!rc) rc = hip_check(hipMemset(c->d_status, 0, 16), "hipMemset");
-    if (!rc) rc = hip_check(hipDeviceSynchronize(), "hipDeviceSynchronize");
-    if (rc) {
-        (void)hipFree(c->d_jump);
-        if (c->d_status) (void)hipFree(c->d_status);
-        delete c;
-        return rc;
-    }
-    P.status = c->d_status;
-    if (P.N <= 128) {
-        uint64_t rows[64 * 4];
-        tmg::build_sb_rows(P.R, P.C, rows);
-        rc = hip_check(hipMalloc(&c->d_sbrows, sizeof rows), "hipMalloc");
-        if (!rc) rc = hip_check(hipMemcpy(c->d_sbrows, rows, sizeof rows, hipMemcpyHostToDevice), "hipMemcpy");
-        if (rc) {
-            (void)hipFree(c->d_jump);
-            (void)hipFree(c->d_status);
-            if (c->d_sbrows) (void)hipFree(c->d_sbrows);
-            delete c;
-            return rc;
-        }
-        P.sb_rows = c->d_sbrows;
-    }
-    *out = c;
-    return 0;
+    return new_ctx(out, device, rows, cols, colours, specials_mask, num_moves, 0);
+}
+
+int tmg_create_scan(tmg_ctx **out, int device, int rows, int cols) {
+    if (!out) return fail(-1, "null output pointer");
+    *out = nullptr;
+    if (rows < 1 || cols < 1) return fail(-2, "board must be at least 1x1");
+    if (rows > 64 || cols > 64 || rows * cols > 512) return fail(-2, "board too large (R,C <= 64, R*C <= 512)");
+    if (2 * rows * cols - rows - cols < 1) return fail(-2, "a 1x1 board has no action");
+    return new_ctx(out, device, rows, cols, 15, 15u, 1, 1);
 }
 
 int tmg_destroy(tmg_ctx *ctx) {
     if (!ctx) return 0;
-    (void)hipFree(ctx->d_jump);
-    (void)hipFree(ctx->d_status);
-    if (ctx->d_sbrows) (void)hipFree(ctx->d_sbrows);
-    for (const auto &x : ctx->spills) {
-        (void)hipFree(x.q);
-        (void)hipFree(x.ws);
-        if (x.rq) (void)hipFree(x.rq);
-    }
-    delete ctx;
+    free_ctx(ctx);
     return 0;
 }
 
@@ -442,11 +376,13 @@ int tmg_spills(tmg_ctx *ctx, uint64_t *count) {
     if (rc) return rc;
     rc = hip_check(hipDeviceSynchronize(), "hipDeviceSynchronize");
     uint64_t tot = 0;
+    std::lock_guard<std::mutex> lock(ctx->mu);
     for (const auto &x : ctx->spills) {
         if (rc) break;
-        tmg::SpillQ h;
-        rc = hip_check(hipMemcpy(&h, x.q, 16, hipMemcpyDeviceToHost), "hipMemcpy");
-        tot += h.total;
+        if (!x.q) continue;
+        unsigned long long t = 0;
+        rc = hip_check(hipMemcpy(&t, &x.q->total, sizeof t, hipMemcpyDeviceToHost), "hipMemcpy");
+        tot += t;
     }
     if (!rc) *count = tot;
     return rc;
@@ -507,7 +443,7 @@ int tmg_reset(tmg_ctx *ctx, int64_t n, int8_t *board, uint64_t *rng, int32_t *ti
 int tmg_reset_onehot(tmg_ctx *ctx, int64_t n, int8_t *board, uint64_t *rng, int32_t *timer, uint64_t *eff,
                      const uint8_t *env_mask, void *onehot, int onehot_dtype, void *stream) {
     if (!board || !rng || !timer || !eff) return fail(-1, "null state buffer");
-    int rc = check_call(ctx, n);
+    int rc = check_full(ctx, n);
     if (rc || n == 0) return rc;
     Params P;
     rc = onehot_params(ctx, onehot, onehot_dtype, P);
@@ -527,7 +463,7 @@ int tmg_step_onehot(tmg_ctx *ctx, int64_t n, int8_t *board, uint64_t *rng, int32
                     int autoreset, void *onehot, int onehot_dtype, void *stream) {
     if (!board || !rng || !timer || !actions || !reward || !n_new || !n_act || !flags || !eff)
         return fail(-1, "null buffer");
-    int rc = check_call(ctx, n);
+    int rc = check_full(ctx, n);
     if (rc || n == 0) return rc;
     Params P;
     rc = onehot_params(ctx, onehot, onehot_dtype, P);
@@ -540,7 +476,11 @@ int tmg_effective(tmg_ctx *ctx, int64_t n, const int8_t *board, uint64_t *eff, v
     if (!board || !eff) return fail(-1, "null buffer");
     int rc = check_call(ctx, n);
     if (rc || n == 0) return rc;
-    return do_effective(ctx, n, board, eff, reinterpret_cast<hipStream_t>(stream));
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    const dim3 grid = tmg::env_grid(n);
+    if (ctx->maxn == 128) tmg::launch_effective128(grid, s, ctx->P, n, board, eff);
+    else tmg::launch_effective512(grid, s, ctx->P, n, board, eff);
+    return hip_check(hipGetLastError(), "kernel launch");
 }
 
 int tmg_onehot_channels(const tmg_ctx *ctx) {
@@ -551,27 +491,14 @@ int tmg_onehot_channels(const tmg_ctx *ctx) {
 
 int tmg_onehot(tmg_ctx *ctx, int64_t n, const int8_t *board, void *out, int out_dtype, void *stream) {
     if (!board || !out) return fail(-1, "null buffer");
-    int rc = check_call(ctx, n);
+    int rc = check_full(ctx, n);
     if (rc || n == 0) return rc;
+    if (out_dtype != TMG_DTYPE_F32 && out_dtype != TMG_DTYPE_U8 && out_dtype != TMG_DTYPE_I32)
+        return fail(-2, "unknown one-hot output dtype");
     int ids[4] = {0, 0, 0, 0};
     const int nsel = onehot_sel((uint32_t)ctx->P.smask, ids);
-    const int4 sel = make_int4(ids[0], ids[1], ids[2], ids[3]);
-    const int64_t cells = n * ctx->P.N;
-    const dim3 grid((unsigned)((cells + 255) / 256)), block(256);
-    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-    switch (out_dtype) {
-    case TMG_DTYPE_F32:
-        hipLaunchKernelGGL(tmg::onehot_kernel<float>, grid, block, 0, s, n, ctx->P.N, ctx->P.k, nsel, sel, board, (float *)out);
-        break;
-    case TMG_DTYPE_U8:
-        hipLaunchKernelGGL(tmg::onehot_kernel<uint8_t>, grid, block, 0, s, n, ctx->P.N, ctx->P.k, nsel, sel, board, (uint8_t *)out);
-        break;
-    case TMG_DTYPE_I32:
-        hipLaunchKernelGGL(tmg::onehot_kernel<int32_t>, grid, block, 0, s, n, ctx->P.N, ctx->P.k, nsel, sel, board, (int32_t *)out);
-        break;
-    default:
-        return fail(-2, "unknown one-hot output dtype");
-    }
+    tmg::launch_onehot(reinterpret_cast<hipStream_t>(stream), n, ctx->P.N, ctx->P.k, nsel,
+                       make_int4(ids[0], ids[1], ids[2], ids[3]), board, out, out_dtype);
     return hip_check(hipGetLastError(), "kernel launch");
 }
 
@@ -581,9 +508,8 @@ int tmg_sample_effective(tmg_ctx *ctx, int64_t n, const uint64_t *eff, uint64_t 
     int rc = check_call(ctx, n);
     if (rc || n == 0) return rc;
     if (first_env < 0) return fail(-2, "first_env must be >= 0");
-    const dim3 grid((unsigned)((n + 255) / 256)), block(256);
-    hipLaunchKernelGGL(tmg::sample_effective_kernel, grid, block, 0, reinterpret_cast<hipStream_t>(stream), n,
-                       ctx->P.W, ctx->P.A, eff, key, first_env, t, actions);
+    tmg::launch_sample_effective(reinterpret_cast<hipStream_t>(stream), n, ctx->P.W, ctx->P.A, eff, key, first_env, t,
+                                 actions);
     return hip_check(hipGetLastError(), "kernel launch");
 }
 
@@ -601,7 +527,6 @@ int tmg_count_states(int device, int rows, int cols, int colours, uint64_t *num_
     if (rc) return rc;
     uint64_t total = 1;
     for (int i = 0; i < rows * cols; i++) total *= (uint64_t)colours;
-    const tmg::CountGeo G = tmg::make_count_geo(rows, cols, colours);
     // >= ~256k threads when there is work for them, runs of >= 1 board
     uint64_t per = total / (1ULL << 18);
     if (per < 1) per = 1;
@@ -611,8 +536,7 @@ int tmg_count_states(int device, int rows, int cols, int colours, uint64_t *num_
     if (rc) return rc;
     rc = hip_check(hipMemset(d, 0, 2 * sizeof(unsigned long long)), "hipMemset");
     if (!rc) {
-        hipLaunchKernelGGL(tmg::count_states_kernel, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, 0, G, total,
-                           per, d);
+        tmg::launch_count_states(rows, cols, colours, total, per, threads, d);
         rc = hip_check(hipGetLastError(), "kernel launch");
     }
     unsigned long long h[2] = {0, 0};
@@ -626,16 +550,32 @@ int tmg_count_states(int device, int rows, int cols, int colours, uint64_t *num_
 
 #if TMG_STAMPS
 // diagnostic build only: copy the per-env phase stamps (uint64 [n][8]) to host memory
-__attribute__((visibility("default"))) int tmg_debug_stamps(uint64_t *host, int64_t n) {
+__attribute__((visibility("default"))) int tmg_debug_stamps(tmg_ctx *ctx, uint64_t *host, int64_t n) {
+    if (!ctx || !ctx->d_stamps) return fail(-1, "no stamps");
     if (n > tmg::kStampEnvs) n = tmg::kStampEnvs;
-    return hip_check(hipMemcpyFromSymbol(host, HIP_SYMBOL(tmg::g_stamps), (size_t)n * tmg::kStampSlots * sizeof(uint64_t), 0,
-                                         hipMemcpyDeviceToHost), "hipMemcpyFromSymbol");
+    int rc = hip_check(hipDeviceSynchronize(), "hipDeviceSynchronize");
+    if (!rc) rc = hip_check(hipMemcpy(host, ctx->d_stamps, (size_t)n * tmg::kStampSlots * 8, hipMemcpyDeviceToHost),
+                            "hipMemcpy");
+    return rc;
+}
+#endif
+
+#if TMG_COVER
+// diagnostic build only: the CV_* branch hit counters of this context
+__attribute__((visibility("default"))) int tmg_debug_cover(tmg_ctx *ctx, uint64_t *host, int n, int clear) {
+    if (!ctx || !ctx->d_cover) return fail(-1, "no cover counters");
+    if (n > tmg::CV_COUNT) n = tmg::CV_COUNT;
+    int rc = hip_check(hipDeviceSynchronize(), "hipDeviceSynchronize");
+    if (!rc) rc = hip_check(hipMemcpy(host, ctx->d_cover, (size_t)n * 8, hipMemcpyDeviceToHost), "hipMemcpy");
+    if (!rc && clear) rc = hip_check(hipMemset(ctx->d_cover, 0, tmg::CV_COUNT * 8), "hipMemset");
+    return rc;
 }
 #endif
 
 int tmg_num_actions(const tmg_ctx *ctx) { return ctx ? ctx->P.A : -1; }
 int tmg_mask_words(const tmg_ctx *ctx) { return ctx ? ctx->P.W : -1; }
 const char *tmg_last_error(void) { return g_err.c_str(); }
-int tmg_abi_version(void) { return 2; }
+int tmg_abi_version(void) { return 3; }
+const char *tmg_build_info(void) { return "src=" TMG_SRC_SHA ";variant=" TMG_VARIANT; }
 
 }  // extern "C"

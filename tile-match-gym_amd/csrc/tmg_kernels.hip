@@ -1,0 +1,144 @@
+// tmg_kernels.hip — kernel instantiations and their host launchers
+// (tmg_launch.h).  Compiled once per translation unit, TMG_TU = 1..6, so the
+// heavy template instantiations build in parallel; each TU registers only its
+// own kernels.
+#include <hip/hip_runtime.h>
+
+#include "tmg_board.hip"
+#include "tmg_launch.h"
+#if TMG_TU == 6
+#include "tmg_aux.hip"      // non-template kernels: one TU only
+#endif
+
+#ifndef TMG_TU
+#error "compile tmg_kernels.hip with -DTMG_TU=1..6"
+#endif
+
+namespace tmg {
+
+namespace {
+
+template <int MAXN, bool GEN, int NB, bool CODD>
+void step_one(dim3 grid, hipStream_t s, const Params &P, const StepArgs &a) {
+    const size_t lds = sizeof(Ws<MAXN, GEN>) * TMG_WPB;
+    hipLaunchKernelGGL((step_kernel<MAXN, GEN, NB, CODD>), grid, dim3(64 * TMG_WPB), lds, s, P, a.n, a.board, a.rng,
+                       a.timer, a.actions, a.reward, a.n_new, a.n_act, a.flags, a.eff, a.trust_eff, a.autoreset);
+}
+
+// scalar-bitboard variants: NB colour planes (sb_planes(k))
+template <bool GEN, bool CODD>
+void step_sb(dim3 grid, hipStream_t s, const Params &P, const StepArgs &a) {
+    switch (sb_planes(P.k)) {
+    case 1: step_one<128, GEN, 1, CODD>(grid, s, P, a); break;
+    case 2: step_one<128, GEN, 2, CODD>(grid, s, P, a); break;
+    case 3: step_one<128, GEN, 3, CODD>(grid, s, P, a); break;
+    default: step_one<128, GEN, 4, CODD>(grid, s, P, a); break;
+    }
+}
+
+template <int MAXN>
+void spill_one(hipStream_t s, const Params &P, const StepArgs &a) {
+    const size_t lds = sizeof(Ws<MAXN, true>);
+    hipLaunchKernelGGL((spill_kernel<MAXN>), dim3(TMG_SPILL_WAVES), dim3(64), lds, s, P, a.n, a.board, a.rng, a.timer,
+                       a.actions, a.reward, a.n_new, a.n_act, a.flags, a.eff, a.trust_eff, a.autoreset);
+}
+
+template <int MAXN, int NB, bool CODD>
+void reset_one(dim3 grid, hipStream_t s, const Params &P, int64_t n, int8_t *board, uint64_t *rng, int32_t *timer,
+               uint64_t *eff, const uint8_t *env_mask, int mask_bits) {
+    const size_t lds = sizeof(Ws<MAXN, false>) * TMG_WPB;
+    hipLaunchKernelGGL((reset_kernel<MAXN, NB, CODD>), grid, dim3(64 * TMG_WPB), lds, s, P, n, board, rng, timer, eff,
+                       env_mask, mask_bits);
+}
+
+template <int MAXN>
+void effective_one(dim3 grid, hipStream_t s, const Params &P, int64_t n, const int8_t *board, uint64_t *eff) {
+    hipLaunchKernelGGL(effective_kernel<MAXN>, grid, dim3(64 * TMG_WPB), sizeof(Ws<MAXN, false>) * TMG_WPB, s, P, n,
+                       board, eff);
+}
+
+}  // namespace
+
+#if TMG_TU == 1
+void launch_step_lean128(bool sb, dim3 grid, hipStream_t s, const Params &P, const StepArgs &a) {
+    if (!sb) step_one<128, false, 0, false>(grid, s, P, a);
+    else if (P.C & 1) step_sb<false, true>(grid, s, P, a);
+    else step_sb<false, false>(grid, s, P, a);
+}
+#endif
+
+#if TMG_TU == 2
+void launch_step_gen128_even(bool sb, dim3 grid, hipStream_t s, const Params &P, const StepArgs &a) {
+    if (sb) step_sb<true, false>(grid, s, P, a);
+    else step_one<128, true, 0, false>(grid, s, P, a);
+}
+void launch_spill128(hipStream_t s, const Params &P, const StepArgs &a) { spill_one<128>(s, P, a); }
+#endif
+
+#if TMG_TU == 3
+void launch_step_gen128_odd(dim3 grid, hipStream_t s, const Params &P, const StepArgs &a) {
+    step_sb<true, true>(grid, s, P, a);
+}
+#endif
+
+#if TMG_TU == 4
+void launch_step512(bool gen, dim3 grid, hipStream_t s, const Params &P, const StepArgs &a) {
+    if (gen) step_one<512, true, 0, false>(grid, s, P, a);
+    else step_one<512, false, 0, false>(grid, s, P, a);
+}
+void launch_spill512(hipStream_t s, const Params &P, const StepArgs &a) { spill_one<512>(s, P, a); }
+void launch_reset512(dim3 grid, hipStream_t s, const Params &P, int64_t n, int8_t *board, uint64_t *rng,
+                     int32_t *timer, uint64_t *eff, const uint8_t *env_mask, int mask_bits) {
+    reset_one<512, 0, false>(grid, s, P, n, board, rng, timer, eff, env_mask, mask_bits);
+}
+void launch_effective512(dim3 grid, hipStream_t s, const Params &P, int64_t n, const int8_t *board, uint64_t *eff) {
+    effective_one<512>(grid, s, P, n, board, eff);
+}
+#endif
+
+#if TMG_TU == 5
+void launch_reset128(bool sb, dim3 grid, hipStream_t s, const Params &P, int64_t n, int8_t *board, uint64_t *rng,
+                     int32_t *timer, uint64_t *eff, const uint8_t *env_mask, int mask_bits) {
+    if (!sb) { reset_one<128, 0, false>(grid, s, P, n, board, rng, timer, eff, env_mask, mask_bits); return; }
+    const bool codd = P.C & 1;
+    switch (sb_planes(P.k)) {
+    case 1: codd ? reset_one<128, 1, true>(grid, s, P, n, board, rng, timer, eff, env_mask, mask_bits)
+                 : reset_one<128, 1, false>(grid, s, P, n, board, rng, timer, eff, env_mask, mask_bits); break;
+    case 2: codd ? reset_one<128, 2, true>(grid, s, P, n, board, rng, timer, eff, env_mask, mask_bits)
+                 : reset_one<128, 2, false>(grid, s, P, n, board, rng, timer, eff, env_mask, mask_bits); break;
+    case 3: codd ? reset_one<128, 3, true>(grid, s, P, n, board, rng, timer, eff, env_mask, mask_bits)
+                 : reset_one<128, 3, false>(grid, s, P, n, board, rng, timer, eff, env_mask, mask_bits); break;
+    default: codd ? reset_one<128, 4, true>(grid, s, P, n, board, rng, timer, eff, env_mask, mask_bits)
+                  : reset_one<128, 4, false>(grid, s, P, n, board, rng, timer, eff, env_mask, mask_bits); break;
+    }
+}
+void launch_effective128(dim3 grid, hipStream_t s, const Params &P, int64_t n, const int8_t *board, uint64_t *eff) {
+    effective_one<128>(grid, s, P, n, board, eff);
+}
+#endif
+
+#if TMG_TU == 6
+void launch_onehot(hipStream_t s, int64_t n, int N, int k, int nsel, int4 sel, const int8_t *board, void *out,
+                   int dtype) {
+    const int64_t cells = n * N;
+    const dim3 grid((unsigned)((cells + 255) / 256)), block(256);
+    switch (dtype) {
+    case 0: hipLaunchKernelGGL(onehot_kernel<float>, grid, block, 0, s, n, N, k, nsel, sel, board, (float *)out); break;
+    case 1: hipLaunchKernelGGL(onehot_kernel<uint8_t>, grid, block, 0, s, n, N, k, nsel, sel, board, (uint8_t *)out); break;
+    default: hipLaunchKernelGGL(onehot_kernel<int32_t>, grid, block, 0, s, n, N, k, nsel, sel, board, (int32_t *)out); break;
+    }
+}
+void launch_sample_effective(hipStream_t s, int64_t n, int W, int A, const uint64_t *eff, uint64_t key,
+                             int64_t first_env, int32_t t, int32_t *actions) {
+    const dim3 grid((unsigned)((n + 255) / 256)), block(256);
+    hipLaunchKernelGGL(sample_effective_kernel, grid, block, 0, s, n, W, A, eff, key, first_env, t, actions);
+}
+void launch_count_states(int R, int C, int k, uint64_t total, uint64_t per, uint64_t threads,
+                         unsigned long long *counts) {
+    const CountGeo G = make_count_geo(R, C, k);
+    hipLaunchKernelGGL(count_states_kernel, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, 0, G, total, per,
+                       counts);
+}
+#endif
+
+}  // namespace tmg

@@ -480,6 +480,7 @@ __device__ __forceinline__ int sb_ensure(const Params &P, WS &w, int lane, const
         }
         if (scan_effective_clean<false>(P, w, lane)) break;   // types all 1, no line
         if (shuffles >= TMG_MAX_SHUFFLES) { fl |= FL_ERR; break; }
+        COVER(CV_SHUFFLE);
         WSYNC();
         shuffle(P, w, lane, g);
         c = sb_codes_from_lds(P, w.brd, lane);
@@ -520,6 +521,7 @@ __device__ __forceinline__ int sb_move(const Params &P, WS &w, int lane, const L
         const SBDet d = sb_detect<NB, CODD>(P, sb_planes_of<NB>(c));
         const int rs = sb_bottom_row(P, d);
         if (rs < 0) break;
+        COVER(CV_SB_LEAN);
         const Pair clr = sb_clear<NB, CODD>(P, d, rs);
         const int tot = popc(clr);
         elim += tot;                                     // R*C - nnz(type) after the resolve (:374)
@@ -728,6 +730,13 @@ __device__ __forceinline__ int sb_simple_step(const Params &P, WS &w, int lane, 
         if (lane == 0) w.sc[SC_NNEW] += popc(pos);
     }
     const int tot = popc(clr);
+#if TMG_COVER
+    if (nonzero(ph | pv)) COVER(CV_SB_LASER);
+    if (nonzero(pbomb)) COVER(CV_SB_PERP_BOMB);
+    if (xb) COVER(CV_SB_ROW_BOMB);
+    if (act) COVER(CV_SB_CLOSURE);
+    if (!nonzero(pos) && !act) COVER(CV_SB_NORMAL);
+#endif
     sb_gravity_refill<CODD, true>(P, w, lane, J, g, clr, tot, c);
     return tot;
 }

@@ -4,21 +4,35 @@ This is the reference-side binding a maintainer would add: the reference has
 no FFI, so the binding replaces the Python Board calls of
 tile_match_env.py:49-124 with the C entry points below.  There is no CPU
 fallback: if the library or a HIP device is missing, every call raises.
+
+Build provenance: the library carries the sha256 of the sources it was built
+from (tmg_build_info); load() recomputes it from the sources in this tree and
+refuses a stale library.  TMG_LIB selects another build (a diagnostic
+variant, or an A/B library); its variant is reported by build_info().
 """
 from __future__ import annotations
 
 import ctypes
+import hashlib
 import os
 
+from . import _buildinfo
+
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.environ.get("TMG_LIB") or os.path.join(_HERE, "_lib", "libtmg.so")   # TMG_LIB: A/B another build
-EXPORTS = ("tmg_create", "tmg_destroy", "tmg_reset", "tmg_step", "tmg_effective",
-           "tmg_num_actions", "tmg_mask_words", "tmg_last_error", "tmg_abi_version",
+DEFAULT_LIB = os.path.join(_HERE, "_lib", "libtmg.so")
+LIB_PATH = os.environ.get("TMG_LIB") or DEFAULT_LIB   # TMG_LIB: a diagnostic or A/B build
+EXPORTS = ("tmg_create", "tmg_create_scan", "tmg_destroy", "tmg_reset", "tmg_step", "tmg_effective",
+           "tmg_num_actions", "tmg_mask_words", "tmg_last_error", "tmg_abi_version", "tmg_build_info",
            "tmg_onehot", "tmg_onehot_channels", "tmg_count_states", "tmg_sample_effective", "tmg_status",
            "tmg_viable", "tmg_spills", "tmg_step_onehot", "tmg_reset_onehot")
 DTYPE_F32, DTYPE_U8, DTYPE_I32 = 0, 1, 2
-ABI_VERSION = 2
+ABI_VERSION = 3
 STATUS_INTERNAL, STATUS_OVERFLOW, STATUS_CALLER = 1, 2, 4
+
+# CV_* branch counters of TMG_COVER builds (tmg_board.hip), in index order
+COVER_NAMES = ("sb_lean", "sb_normal", "sb_laser", "sb_perp_bomb", "sb_row_bomb", "sb_closure", "sb_fallback",
+               "lds_normal", "lds_laser", "lds_bomb", "lds_fallback", "serial_step", "serial_act", "serial_cookie",
+               "combo", "spill", "spill_run", "shuffle", "reject", "fast")
 
 SPECIAL_BITS = {"cookie": 1, "vertical_laser": 2, "horizontal_laser": 4, "bomb": 8}
 FLAG_DONE, FLAG_COMBO, FLAG_SHUFFLED, FLAG_RESET, FLAG_OVERFLOW, FLAG_ERROR = 1, 2, 4, 8, 0x40, 0x80
@@ -44,6 +58,9 @@ def load():
                        "(or __graft_entry__.build()); there is no CPU fallback")
     L = ctypes.CDLL(LIB_PATH)
     L.tmg_create.argtypes = [ctypes.POINTER(P), I, I, I, I, ctypes.c_uint32, I]
+    L.tmg_create_scan.argtypes = [ctypes.POINTER(P), I, I, I]
+    L.tmg_build_info.argtypes = []
+    L.tmg_build_info.restype = ctypes.c_char_p
     L.tmg_destroy.argtypes = [P]
     L.tmg_reset.argtypes = [P, I64, P, P, P, P, P, P]
     L.tmg_step.argtypes = [P, I64, P, P, P, P, P, P, P, P, P, I, I, P]
@@ -62,15 +79,36 @@ def load():
     L.tmg_spills.argtypes = [P, ctypes.POINTER(ctypes.c_uint64)]
     L.tmg_step_onehot.argtypes = [P, I64, P, P, P, P, P, P, P, P, P, I, I, P, I, P]
     L.tmg_reset_onehot.argtypes = [P, I64, P, P, P, P, P, P, I, P]
-    for name in ("tmg_create", "tmg_destroy", "tmg_reset", "tmg_step", "tmg_effective",
+    for name in ("tmg_create", "tmg_create_scan", "tmg_destroy", "tmg_reset", "tmg_step", "tmg_effective",
                  "tmg_num_actions", "tmg_mask_words", "tmg_abi_version", "tmg_onehot", "tmg_onehot_channels",
                  "tmg_sample_effective", "tmg_status", "tmg_viable", "tmg_spills", "tmg_step_onehot", "tmg_reset_onehot",
                  "tmg_count_states"):
         getattr(L, name).restype = I
     if L.tmg_abi_version() != ABI_VERSION:
         raise TmgError("libtmg.so ABI version mismatch; rebuild it")
+    info = _parse_info(L.tmg_build_info().decode())
+    want = _buildinfo.source_hash()
+    if want is not None and info.get("src") != want:
+        raise TmgError(f"{LIB_PATH} was built from other sources (src={info.get('src')}, tree={want}): "
+                       "stale build, run `make -C tile-match-gym_amd -B`")
+    if LIB_PATH == DEFAULT_LIB and info.get("variant") != "product":
+        raise TmgError(f"{LIB_PATH} is a {info.get('variant')!r} build, not the product library")
     _lib = L
     return L
+
+
+def _parse_info(s: str) -> dict:
+    return dict(kv.split("=", 1) for kv in s.split(";") if "=" in kv)
+
+
+def build_info() -> dict:
+    """{'src': sha256 of the sources built in, 'variant': ..., 'path': ..., 'so_sha256': ...}."""
+    L = load()
+    info = _parse_info(L.tmg_build_info().decode())
+    with open(LIB_PATH, "rb") as f:
+        info["so_sha256"] = hashlib.sha256(f.read()).hexdigest()
+    info["path"] = LIB_PATH
+    return info
 
 
 def check(rc: int):
@@ -89,13 +127,18 @@ def specials_mask(colourless_specials, colour_specials) -> int:
 
 
 class Context:
-    """Owns a tmg_ctx (shape / colours / specials / episode length on one device)."""
+    """Owns a tmg_ctx (shape / colours / specials / episode length on one device).
+    scan_only=True: tmg_create_scan, a context for effective() on any shape."""
 
-    def __init__(self, device_index: int, rows: int, cols: int, colours: int, smask: int, num_moves: int):
+    def __init__(self, device_index: int, rows: int, cols: int, colours: int = 0, smask: int = 0,
+                 num_moves: int = 1, scan_only: bool = False):
         L = load()
         h = P()
-        check(L.tmg_create(ctypes.byref(h), int(device_index), int(rows), int(cols), int(colours),
-                           int(smask), int(num_moves)))
+        if scan_only:
+            check(L.tmg_create_scan(ctypes.byref(h), int(device_index), int(rows), int(cols)))
+        else:
+            check(L.tmg_create(ctypes.byref(h), int(device_index), int(rows), int(cols), int(colours),
+                               int(smask), int(num_moves)))
         self._h = h
         self.num_actions = L.tmg_num_actions(h)
         self.mask_words = L.tmg_mask_words(h)
@@ -154,9 +197,34 @@ class Context:
     def onehot(self, n, board, out, out_dtype, stream):
         check(load().tmg_onehot(self._h, int(n), board, out, int(out_dtype), stream))
 
+    def cover(self, clear: bool = False):
+        """CV_* branch hit counters (diagnostic TMG_COVER builds only: tmg_debug_cover)."""
+        L = load()
+        fn = getattr(L, "tmg_debug_cover", None)
+        if fn is None:
+            raise TmgError(f"{LIB_PATH} is not a TMG_COVER build")
+        import numpy as np
+        out = np.zeros(32, np.uint64)
+        fn.argtypes = [P, P, I, I]
+        fn.restype = I
+        check(fn(self._h, out.ctypes.data, 32, int(clear)))
+        return out
+
     def sample_effective(self, n, eff, key, first_env, t, actions, stream):
         check(load().tmg_sample_effective(self._h, int(n), eff, int(key) & 0xFFFFFFFFFFFFFFFF, int(first_env),
                                           int(t), actions, stream))
+
+
+_SCAN_CTX = {}
+
+
+def scan_context(device_index: int, rows: int, cols: int) -> "Context":
+    """One cached tmg_create_scan context per (device, rows, cols)."""
+    key = (int(device_index), int(rows), int(cols))
+    c = _SCAN_CTX.get(key)
+    if c is None:
+        c = _SCAN_CTX[key] = Context(key[0], key[1], key[2], scan_only=True)
+    return c
 
 
 def viable(rows: int, cols: int, colours: int) -> bool:

@@ -13,7 +13,7 @@ from collections import OrderedDict
 import numpy as np
 
 try:  # pragma: no cover - exercised only where gymnasium is installed
-    from gymnasium.spaces import Box, Dict, Discrete  # noqa: F401
+    from gymnasium.spaces import Box, Dict, Discrete, MultiDiscrete  # noqa: F401
     HAVE_GYMNASIUM = True
 except Exception:  # gymnasium absent
     HAVE_GYMNASIUM = False
@@ -57,6 +57,29 @@ except Exception:  # gymnasium absent
 
         def __eq__(self, other):
             return isinstance(other, Discrete) and other.n == self.n and other.start == self.start
+
+    class MultiDiscrete(_Space):
+        """gymnasium.spaces.MultiDiscrete: one Discrete(nvec[i]) per entry, the
+        batched form of Discrete (gymnasium.vector.utils.batch_space)."""
+
+        def __init__(self, nvec, dtype=np.int64, seed=None, start=None):
+            self.nvec = np.asarray(nvec, dtype=dtype)
+            self.start = np.zeros_like(self.nvec) if start is None else np.asarray(start, dtype=dtype)
+            super().__init__(self.nvec.shape, dtype, seed)
+
+        def sample(self, mask=None):
+            return (self.start + self.np_random.integers(0, self.nvec)).astype(self.dtype)
+
+        def contains(self, x):
+            x = np.asarray(x)
+            return x.shape == self.shape and bool(np.all(x >= self.start)) and bool(np.all(x < self.start + self.nvec))
+
+        def __repr__(self):
+            return f"MultiDiscrete({self.nvec})"
+
+        def __eq__(self, other):
+            return isinstance(other, MultiDiscrete) and np.array_equal(other.nvec, self.nvec) and \
+                np.array_equal(other.start, self.start)
 
     class Box(_Space):
         def __init__(self, low, high, shape=None, dtype=np.float32, seed=None):

@@ -175,32 +175,49 @@ class Board:
 
     def effective_actions(self) -> List[int]:
         """Ascending actions a with is_move_effective(board, *action_to_coords[a])."""
-        d = self._buffers()
-        self._upload(d)
-        d["ctx"].effective(1, d["board"].data_ptr(), d["eff"].data_ptr(), self._stream(d))
-        w = d["eff"][0].cpu().numpy().view(np.uint64)
-        bits = np.unpackbits(w.view(np.uint8), bitorder="little")[:self.num_actions]
-        return [int(a) for a in np.nonzero(bits)[0]]
+        return _effective_actions(self.board, self._device)
 
     def possible_move(self, grid=None) -> bool:                              # board.py:558-569
-        if grid is None:
-            return bool(self.effective_actions())
-        return bool(Board(self.num_rows, self.num_cols, self.num_colours, self.colourless_specials,
-                          self.colour_specials, board=np.asarray(grid), device=self._device).effective_actions())
+        return bool(_effective_actions(self.board if grid is None else np.asarray(grid), self._device))
+
+
+def _effective_actions(board, device=None) -> List[int]:
+    """is_move_effective (board.py:735-787) for every action of one board of
+    any shape, on the device (effective_kernel) through a cached scan-only
+    context (tmg_create_scan: no viability test, like the reference, which
+    accepts any board here)."""
+    b = np.asarray(board)
+    if b.ndim == 2:                                                          # board.py:64-74 promotion
+        b = np.array([b, np.ones_like(b)])
+    if device is None:
+        if not torch.cuda.is_available():
+            raise _native.TmgError("is_move_effective needs a HIP device (no CPU fallback)")
+        device = torch.device("cuda", torch.cuda.current_device())
+    device = torch.device(device)
+    idx = device.index if device.index is not None else 0
+    R, C = b.shape[1], b.shape[2]
+    ctx = _native.scan_context(idx, R, C)
+    d_board = torch.from_numpy(np.ascontiguousarray(b, dtype=np.int8)).unsqueeze(0).to(device)
+    d_eff = torch.zeros((1, ctx.mask_words), dtype=torch.int64, device=device)
+    ctx.effective(1, d_board.data_ptr(), d_eff.data_ptr(), torch.cuda.current_stream(device).cuda_stream)
+    w = d_eff[0].cpu().numpy().view(np.uint64)
+    bits = np.unpackbits(w.view(np.uint8), bitorder="little")[:ctx.num_actions]
+    return [int(a) for a in np.nonzero(bits)[0]]
 
 
 def is_move_effective(board, coord1, coord2) -> bool:
     """board.py:735-787 on the device (effective_kernel) for one board and one
-    pair of adjacent coords.  The board may hold any colours / types; the
-    answer does not depend on the colour count or the enabled specials."""
+    pair of adjacent coords.  The board may hold any colours / types and have
+    any shape; the answer does not depend on the colour count or the enabled
+    specials."""
     b = np.asarray(board)
-    R, C = b.shape[1], b.shape[2]
-    bd = Board(R, C, 4, [], [], board=b)
+    R, C = b.shape[-2], b.shape[-1]
+    table = {c: a for a, c in enumerate(action_to_coords(R, C))}
     key = (tuple(int(x) for x in coord1), tuple(int(x) for x in coord2))
-    a = bd._coord_to_action.get(key)
+    a = table.get(key)
     if a is None:
-        a = bd._coord_to_action[(key[1], key[0])]
-    return a in bd.effective_actions()
+        a = table[(key[1], key[0])]
+    return a in _effective_actions(b)
 
 
 class TileMatchEnv(_EnvBase):

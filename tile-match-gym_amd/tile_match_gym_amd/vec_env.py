@@ -239,11 +239,14 @@ class TileMatchVecEnv:
         (tmg_sample_effective; counter-based in (key, first_env + env, t), so a
         shard passing its global offset as first_env picks the same actions as
         the unsharded batch).  The sampled actions stay in self.actions."""
+        # a mask from tmg_effective (hand-edited boards) may sit beside a line
+        # on the board, so that step runs untrusted (tmg.h, trust_eff)
+        trust = int(self._eff_valid)
         if not self._eff_valid:
             self.compute_effective()
         if self.actions is None:
             self.actions = torch.zeros(self.num_envs, dtype=torch.int32, device=self.device)
-        trust, auto = 1, int(self.autoreset)
+        auto = int(self.autoreset)
         act = self.actions.data_ptr()
         if not self._streams:
             s = self._stream()

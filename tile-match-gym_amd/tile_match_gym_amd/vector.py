@@ -30,7 +30,7 @@ import numpy as np
 import torch
 
 from . import _native
-from .spaces import Box, Dict, Discrete
+from .spaces import Box, Dict, Discrete, MultiDiscrete
 from .vec_env import TileMatchVecEnv
 
 
@@ -61,11 +61,13 @@ class TileMatchVectorEnv:
         self.single_observation_space = Dict({"board": Box(low=low, high=high, shape=(2, R, C), dtype=np.int32),
                                               "num_moves_left": Discrete(num_moves + 1)})
         self.single_action_space = Discrete(self.vec.num_actions)
+        # batched as gymnasium.vector.utils.batch_space does: Box -> stacked Box,
+        # Discrete(n) -> MultiDiscrete([n] * num_envs)
         self.observation_space = Dict({
             "board": Box(low=np.broadcast_to(low, (num_envs, 2, R, C)), high=np.broadcast_to(high, (num_envs, 2, R, C)),
                          shape=(num_envs, 2, R, C), dtype=np.int32),
-            "num_moves_left": Box(low=0, high=num_moves, shape=(num_envs,), dtype=np.int64)})
-        self.action_space = Box(low=0, high=self.vec.num_actions - 1, shape=(num_envs,), dtype=np.int64)
+            "num_moves_left": MultiDiscrete(np.full(num_envs, num_moves + 1, dtype=np.int64))})
+        self.action_space = MultiDiscrete(np.full(num_envs, self.vec.num_actions, dtype=np.int64))
         self._autoreset = torch.zeros(num_envs, dtype=torch.bool, device=self.device)
         self._bits = torch.arange(64, device=self.device, dtype=torch.int64)
 

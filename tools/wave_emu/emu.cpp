@@ -203,13 +203,24 @@ static void run_blocks(int64_t n, size_t lds, F kernel) {
 
 static uint64_t g_sbrows[64 * 4];
 static uint32_t g_status[4];
-static tmg::SpillQ g_spill;
+static std::vector<int64_t> g_spill_buf;          // a SpillQ with room for every env of the call
+static unsigned long long g_spill_total = 0;
+static unsigned long long g_cover[tmg::CV_COUNT];
 static std::vector<unsigned char> g_spill_ws(sizeof(tmg::WsSerialBig<512>) * TMG_SPILL_WAVES);
+static tmg::SpillQ *spill_queue(int64_t n) {
+    const size_t words = (sizeof(tmg::SpillQ) + (size_t)n * 8 + 7) / 8;
+    g_spill_buf.assign(words, 0);
+    tmg::SpillQ *q = reinterpret_cast<tmg::SpillQ *>(g_spill_buf.data());
+    q->cap = n;
+    q->total = 0;
+    return q;
+}
 static tmg::Params make_params(int R, int C, int k, int smask, int moves, const uint64_t *jump) {
     tmg::Params P = tmg::make_params(R, C, k, smask, moves, jump);
     P.status = g_status;
-    P.spill = &g_spill;
+    P.spill = nullptr;
     P.spill_ws = g_spill_ws.data();
+    P.cover = g_cover;
     if (P.N <= 128) {
         tmg::build_sb_rows(R, C, g_sbrows);
         P.sb_rows = g_sbrows;
@@ -220,10 +231,7 @@ static tmg::Params make_params(int R, int C, int k, int smask, int moves, const 
 static uint64_t g_jump[256];
 static bool g_jump_init = false;
 
-static bool sb_ok(const tmg::Params &P) {
-    const char *v = getenv("TMG_SB");
-    return P.N <= 128 && P.C <= 63 && !(v && v[0] == '0');
-}
+static bool sb_ok(const tmg::Params &P) { return P.N <= 128 && P.C <= 63; }
 
 // step variants as tmg_capi.hip's do_step: one wave per env
 struct EmuStep {
@@ -286,37 +294,6 @@ static void emu_do_reset(const tmg::Params &P, int64_t n, int8_t *board, uint64_
     }
 }
 
-template <int M, int B, bool O>
-struct RqTag {
-    static constexpr int maxn = M, nb = B;
-    static constexpr bool codd = O;
-};
-template <class F>
-static void template_dispatch(const tmg::Params &P, F run) {
-    if (P.N > 128) { run(RqTag<512, 0, false>{}); return; }
-    if (!sb_ok(P)) { run(RqTag<128, 0, false>{}); return; }
-    const bool o = P.C & 1;
-    switch (tmg::sb_planes(P.k)) {
-    case 1: if (o) run(RqTag<128, 1, true>{}); else run(RqTag<128, 1, false>{}); break;
-    case 2: if (o) run(RqTag<128, 2, true>{}); else run(RqTag<128, 2, false>{}); break;
-    case 3: if (o) run(RqTag<128, 3, true>{}); else run(RqTag<128, 3, false>{}); break;
-    default: if (o) run(RqTag<128, 4, true>{}); else run(RqTag<128, 4, false>{}); break;
-    }
-}
-
-// the deferred autoresets through the queue, as tmg_capi.hip's do_step
-static std::vector<unsigned char> g_rq;
-static void emu_reset_queued(const tmg::Params &P, int64_t n, int8_t *board, uint64_t *rng, int32_t *timer,
-                             uint64_t *eff) {
-    const int64_t g = n < 64 ? n : 64;
-    auto run = [&](auto tag) {
-        constexpr int MAXN = decltype(tag)::maxn, NB = decltype(tag)::nb;
-        constexpr bool CODD = decltype(tag)::codd;
-        run_grid(g, sizeof(tmg::Ws<MAXN, false>), [&] { tmg::reset_queue_kernel<MAXN, NB, CODD>(P, board, rng, timer, eff); });
-    };
-    template_dispatch(P, run);
-}
-
 extern "C" {
 
 int emu_step(int R, int C, int k, int smask, int moves, int64_t n, int8_t *board, uint64_t *rng, int32_t *timer,
@@ -324,53 +301,42 @@ int emu_step(int R, int C, int k, int smask, int moves, int64_t n, int8_t *board
              int trust_eff, int autoreset) {
     if (!g_jump_init) { tmg::build_jump_table(g_jump); g_jump_init = true; }
     tmg::Params P = make_params(R, C, k, smask, moves, g_jump);
-    g_rq.assign(sizeof(tmg::ResetQ) + (size_t)n * sizeof(int64_t), 0);
-    P.resetq = reinterpret_cast<tmg::ResetQ *>(g_rq.data());
+    P.spill = spill_queue(n);
     EmuStep S;
     S.P = &P; S.n = n; S.board = board; S.rng = rng; S.timer = timer; S.actions = actions; S.reward = reward;
     S.n_new = n_new; S.n_act = n_act; S.flags = flags; S.eff = eff; S.trust_eff = trust_eff; S.autoreset = autoreset;
     const bool lean = smask == 0 && trust_eff;
     S.autoreset = autoreset ? 1 : 0;
+    // as tmg_capi.hip's do_step: the general and 512-cell kernels leave
+    // finished boards to a reset launch masked by FL_RESET
+    const int deferred = S.autoreset && (P.N > 128 || !lean || TMG_LEAN_DEFER);
+    if (deferred) S.autoreset = 2;
     if (P.N <= 128) {
-        if (sb_ok(P)) {
-            if (lean) {
-                const int deferred = TMG_LEAN_DEFER ? S.autoreset : 0;    // as tmg_capi.hip's do_step
-                if (deferred) S.autoreset = 2;
-                if (P.C & 1) emu_step_sb<false, true>(S); else emu_step_sb<false, false>(S);
-                if (deferred) emu_reset_queued(P, n, board, rng, timer, eff);
-            }
-            else {
-                // general kernel: autoreset deferred to a FL_RESET-masked reset, as tmg_capi.hip
-                const int deferred = S.autoreset;
-                if (deferred) S.autoreset = 2;
-                if (P.C & 1) emu_step_sb<true, true>(S); else emu_step_sb<true, false>(S);
-                emu_spill<128>(S);
-                if (deferred) emu_reset_queued(P, n, board, rng, timer, eff);
-            }
-        } else if (lean) {
-            const int deferred = TMG_LEAN_DEFER ? S.autoreset : 0;
-            if (deferred) S.autoreset = 2;
-            emu_step_kernel<128, false, 0, false>(S);
-            if (deferred) emu_reset_queued(P, n, board, rng, timer, eff);
+        if (lean) {
+            if (!sb_ok(P)) emu_step_kernel<128, false, 0, false>(S);
+            else if (P.C & 1) emu_step_sb<false, true>(S);
+            else emu_step_sb<false, false>(S);
         } else {
-            emu_step_kernel<128, true, 0, false>(S);
+            if (!sb_ok(P)) emu_step_kernel<128, true, 0, false>(S);
+            else if (P.C & 1) emu_step_sb<true, true>(S);
+            else emu_step_sb<true, false>(S);
             emu_spill<128>(S);
         }
-        return 0;
-    }
-    // 512-cell kernels: deferred regeneration by a reset launch masked by FL_RESET
-    const int deferred = S.autoreset;
-    if (deferred) S.autoreset = 2;
-    if (lean) emu_step_kernel<512, false, 0, false>(S);
-    else {
+    } else if (lean) {
+        emu_step_kernel<512, false, 0, false>(S);
+    } else {
         emu_step_kernel<512, true, 0, false>(S);
         emu_spill<512>(S);
     }
-    if (deferred) emu_reset_queued(P, n, board, rng, timer, eff);
+    g_spill_total += P.spill->total;
+    if (deferred) emu_do_reset(P, n, board, rng, timer, eff, flags, tmg::FL_RESET);
     return 0;
 }
 
-unsigned long long emu_spills(void) { return g_spill.total; }
+unsigned long long emu_spills(void) { return g_spill_total; }
+void emu_cover(unsigned long long *out, int clear) {
+    for (int i = 0; i < tmg::CV_COUNT; i++) { out[i] = g_cover[i]; if (clear) g_cover[i] = 0; }
+}
 unsigned emu_status(void) { return (g_status[0] ? 1u : 0u) | (g_status[1] ? 2u : 0u) | (g_status[2] ? 4u : 0u); }
 
 int emu_reset(int R, int C, int k, int smask, int moves, int64_t n, int8_t *board, uint64_t *rng, int32_t *timer,

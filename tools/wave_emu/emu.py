@@ -23,7 +23,16 @@ def load(asan=False):
     L.emu_effective.argtypes = [I, I, I, I, I64, P, P]
     L.emu_spills.restype = ctypes.c_ulonglong
     L.emu_status.restype = ctypes.c_uint
+    L.emu_cover.argtypes = [P, I]
+    L.emu_cover.restype = None
     return L
+
+
+def cover(L, clear=False):
+    """The CV_* branch counters of the emulated kernels (the emulator is built with TMG_COVER)."""
+    out = np.zeros(32, np.uint64)
+    L.emu_cover(out.ctypes.data, int(clear))
+    return out
 
 
 class EmuBatch:
