@@ -4,6 +4,7 @@
 #   STAGE=deep  bash scripts/gpu_r03.sh   # the deep rollouts vs the oracle + the TMG_COVER branch counts
 #   STAGE=bench bash scripts/gpu_r03.sh   # c2 / c3 / c5 bench lines with the CPU baseline + driver window
 #   STAGE=prof  bash scripts/gpu_r03.sh   # rocprofv3 --kernel-trace --stats of the c2 / c3 / c5 benches
+#   STAGE=all   bash scripts/gpu_r03.sh   # tests, deep, bench
 # Each GPU step has its own time limit; the script stops at the first failure.
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 TAG=${TAG:-r03}
@@ -34,6 +35,9 @@ bench)
   done
   timeout -k 10 300 python bench.py --steps 20 --warmup 5 --no-cpu-baseline > $OUT/c2_driver_window_bench.log 2>&1 || exit 1
   tail -1 $OUT/c2_driver_window_bench.log | cut -c1-200
+  ;;
+all)
+  STAGE=tests bash scripts/gpu_r03.sh && STAGE=deep bash scripts/gpu_r03.sh && STAGE=bench bash scripts/gpu_r03.sh
   ;;
 prof)
   for c in c2 c3 c5; do

@@ -313,9 +313,13 @@ __device__ __forceinline__ Pair sb_clear(const Params &P, const SBDet &d, int rs
 // TYPES: move the type plane too (boards with specials); the refilled cells
 // become normal tiles (type 1).  Without it the type plane is all 1 and stays.
 template <bool CODD, bool TYPES = false, class WS>
-__device__ __forceinline__ void sb_gravity_refill(const Params &P, WS &w, int lane, const LaneJump &J, Rng &g,
+__device__ __forceinline__ void sb_gravity_refill(const Params &P, WS &w, int lane_, const LaneJump &J, Rng &g,
                                                   const Pair E, int total, SBC &c) {
     const int N = P.N, C = P.C;
+    // the refill draws first, while nothing per-lane is live beside the RNG
+    // (the jump-ahead's 128-bit products need the registers)
+    draw_colours<true>(P, lane_, J, g, total, w.u.draw, w.trash);
+    const int lane = loop_lane(lane_);           // the per-lane column masks below are rebuilt per call
     int8_t *col = w.brd, *typ = w.brd + N;
     const int q0 = 2 * lane, q1 = q0 + 1;
     const int r0 = div_c(P, q0), c0 = q0 - r0 * C;
@@ -343,15 +347,13 @@ __device__ __forceinline__ void sb_gravity_refill(const Params &P, WS &w, int la
     const bool e0 = v0 && ((E.a >> lane) & 1ULL), e1 = v1 && ((E.b >> lane) & 1ULL);
     const bool n0 = v0 && r0 < ec0, n1 = v1 && r1 < ec1;   // refilled after gravity
     const uint64_t NA = __ballot(n0), NBm = __ballot(n1);
-    const uint64_t lt = lanemask_lt(lane);
-    const int rank0 = __popcll(NA & lt) + __popcll(NBm & lt);
+    const int rank0 = popc_below(NA) + popc_below(NBm);
     const int rank1 = rank0 + (n0 ? 1 : 0);
     int8_t y0 = 1, y1 = 1;
     if constexpr (TYPES) {
         y0 = typ[v0 ? q0 : 0];
         y1 = typ[v1 ? q1 : 0];
     }
-    draw_colours(P, lane, J, g, total, w.u.draw, w.trash);
     WSYNC();
     const int8_t d0 = (int8_t)w.u.draw[n0 ? rank0 : 0], d1 = (int8_t)w.u.draw[n1 ? rank1 : 0];
     WFENCE();
@@ -410,7 +412,7 @@ __device__ __forceinline__ void sb_draw_rows(const Params &P, WS &w, int lane, c
     const bool rej = (ok0 && (uint32_t)m0 < P.thr) || (ok1 && (uint32_t)m1 < P.thr);
     if (P.thr != 0u && (rbuf || __ballot(rej) != 0ULL)) {
         // Lemire rejection somewhere: exact serial replay
-        draw_colours(P, lane, J, g, M, w.u.draw, w.trash);
+        draw_colours<true>(P, lane, J, g, M, w.u.draw, w.trash);
         WSYNC();
         c.a = inA ? (int)w.u.draw[2 * lane] - 1 : c.a;
         c.b = inB ? (int)w.u.draw[2 * lane + 1] - 1 : c.b;

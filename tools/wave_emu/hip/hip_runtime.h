@@ -61,6 +61,18 @@ inline unsigned atomicAdd(unsigned *p, unsigned v) { unsigned o = *p; *p += v; r
 inline unsigned long long atomicAdd(unsigned long long *p, unsigned long long v) { unsigned long long o = *p; *p += v; return o; }
 inline void __threadfence() {}
 
+inline unsigned emu_mbcnt_lo(unsigned m, unsigned acc) {
+    const unsigned l = emu_thread_idx().x;
+    return acc + (unsigned)__builtin_popcount(m & (l >= 32 ? 0xffffffffu : ((1u << l) - 1u)));
+}
+inline unsigned emu_mbcnt_hi(unsigned m, unsigned acc) {
+    const unsigned l = emu_thread_idx().x;
+    return acc + (unsigned)__builtin_popcount(m & (l <= 32 ? 0u : ((1u << (l - 32)) - 1u)));
+}
+#define __builtin_amdgcn_mbcnt_lo(m, a) emu_mbcnt_lo((m), (a))
+#define __builtin_amdgcn_mbcnt_hi(m, a) emu_mbcnt_hi((m), (a))
+#define TMG_OPAQUE_V(x) ((void)0)
+
 #define TMG_CONST_AS
 #define TMG_KEEP_V3(x, y, z) ((void)0)
 #define TMG_SMEM_DECL(name) unsigned char *name = emu_smem()
