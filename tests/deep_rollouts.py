@@ -6,10 +6,10 @@ seeds, same action streams):
 * tests/test_gpu_deep.py runs them on the product library against the CPU
   oracle (oracle/tmg_oracle.c, pinned by the reference's goldens), every field
   of every env at every step;
-* `python tests/deep_rollouts.py --cover OUT.json` (a child process with
-  TMG_LIB pointing at the TMG_COVER diagnostic build, libtmg_cover.so) runs
-  them on the GPU only and writes the per-branch hit counters (CV_* in
-  tmg_board.hip), so the test can show that every cascade-step form — the
+* cover_counts() runs them on the GPU only with the TMG_COVER diagnostic
+  build (libtmg_cover.so, loaded beside the product library) and returns the
+  per-branch hit counters (CV_* in tmg_board.hip), so the test can show that
+  every cascade-step form — the
   bitboard normal / laser / perpendicular-bomb / row-bomb / closure steps, the
   512-cell LDS forms, the lane-0 fallback, the spill path — ran on exactly the
   trajectories the parity run checked.
@@ -54,7 +54,10 @@ def seed_base(name):
     return 100_000 * (1 + sorted(CONFIGS).index(name))
 
 
-def run(name, device="cuda:0", check=None, threads=16):
+COVER_LIB = os.path.join(ROOT, "tile-match-gym_amd", "tile_match_gym_amd", "_lib", "libtmg_cover.so")
+
+
+def run(name, device="cuda:0", check=None, threads=16, lib_path=None):
     """Roll config `name` out on the device.  check(t, env, ref) is called
     after every step when given (then the oracle runs beside it)."""
     import torch
@@ -63,7 +66,8 @@ def run(name, device="cuda:0", check=None, threads=16):
     R, C, k, sm, n, steps, policy = CONFIGS[name]
     cl, co = specials(sm)
     base = seed_base(name)
-    env = TileMatchVecEnv(n, R, C, k, 30, cl, co, seeds=range(base, base + n), device=device, groups=2)
+    env = TileMatchVecEnv(n, R, C, k, 30, cl, co, seeds=range(base, base + n), device=device, groups=2,
+                          lib_path=lib_path)
     ref = None
     if check is not None:
         from oracle import oracle as orc
@@ -93,23 +97,29 @@ def run(name, device="cuda:0", check=None, threads=16):
     return env
 
 
+def cover_counts(names=None):
+    """{name: {"counts": {CV name: hits}, "status": ..., ...}} from the TMG_COVER build."""
+    from tile_match_gym_amd import _native
+    info = _native.build_info(COVER_LIB)
+    if info.get("variant") != "cover":
+        raise RuntimeError(f"{COVER_LIB} is not the TMG_COVER build ({info})")
+    res = {"build": info, "names": list(_native.COVER_NAMES), "configs": {}}
+    for name in names or sorted(CONFIGS):
+        t0 = time.time()
+        env = run(name, lib_path=COVER_LIB)
+        c = env.ctx.cover()
+        res["configs"][name] = {"counts": {nm: int(c[i]) for i, nm in enumerate(_native.COVER_NAMES)},
+                                "status": env.status(), "seconds": round(time.time() - t0, 2), "spec": CONFIGS[name]}
+        env.close()
+    return res
+
+
 def main():
     out = sys.argv[sys.argv.index("--cover") + 1]
-    names = [a for a in sys.argv[1:] if a in CONFIGS] or sorted(CONFIGS)
-    from tile_match_gym_amd import _native
-    info = _native.build_info()
-    if info.get("variant") != "cover":
-        raise SystemExit(f"deep_rollouts --cover needs TMG_LIB=libtmg_cover.so (got {info})")
-    res = {"build": info, "names": list(_native.COVER_NAMES), "configs": {}}
-    for name in names:
-        t0 = time.time()
-        env = run(name)
-        c = env.ctx.cover()
-        st = env.status()
-        res["configs"][name] = {"counts": {nm: int(c[i]) for i, nm in enumerate(_native.COVER_NAMES)},
-                                "status": st, "seconds": round(time.time() - t0, 2), "spec": CONFIGS[name]}
-        print(name, res["configs"][name], flush=True)
-        env.close()
+    names = [a for a in sys.argv[1:] if a in CONFIGS] or None
+    res = cover_counts(names)
+    for name, c in res["configs"].items():
+        print(name, c, flush=True)
     with open(out, "w") as f:
         json.dump(res, f, indent=1)
 

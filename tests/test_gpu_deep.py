@@ -10,18 +10,14 @@ Reference: board.py:269-327 (process_colour_lines), :429-458
 (combination_match)."""
 import json
 import os
-import subprocess
-import sys
 
 import numpy as np
 import pytest
 
-from deep_rollouts import CONFIGS, run
+from deep_rollouts import CONFIGS, COVER_LIB, cover_counts, run
 
 pytestmark = pytest.mark.gpu
 
-ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-COVER_LIB = os.path.join(ROOT, "tile-match-gym_amd", "tile_match_gym_amd", "_lib", "libtmg_cover.so")
 
 FIELDS = ("board", "rng", "timer", "eff", "reward", "n_new", "n_act", "flags")
 
@@ -62,15 +58,11 @@ REQUIRED = {
 }
 
 
-def test_cascade_branch_coverage(tmp_path):
-    """The TMG_COVER build on the same trajectories: per-branch hit counts."""
+def test_cascade_branch_coverage():
+    """The TMG_COVER build (loaded beside the product library, its own
+    contexts and kernels) on the same trajectories: per-branch hit counts."""
     assert os.path.exists(COVER_LIB), "build() makes libtmg_cover.so"
-    out = tmp_path / "cover.json"
-    env = dict(os.environ, TMG_LIB=COVER_LIB)
-    r = subprocess.run([sys.executable, os.path.join(ROOT, "tests", "deep_rollouts.py"), "--cover", str(out)],
-                       env=env, cwd=ROOT, timeout=600, capture_output=True, text=True)
-    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
-    res = json.loads(out.read_text())
+    res = cover_counts()
     keep = os.environ.get("TMG_COVER_OUT")
     if keep:
         with open(keep, "w") as f:

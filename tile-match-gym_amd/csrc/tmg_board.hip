@@ -853,7 +853,30 @@ __device__ __forceinline__ int first_line_row(const Params &P, const WS &w, int 
     const int8_t *col = w.brd, *typ = w.brd + N;
     const int last = min((lim + 1) * C, N) - 1;          // highest cell that may anchor a line
     int best = -1, stop = -2;                            // stop: lowest pass still to scan, once found
-    if constexpr (!ROLL || WS::NP <= 2) {
+    if constexpr (!ROLL && WS::NP > 2) {
+        // 512-cell reset kernel: unrolled (the passes' loads overlap), the cell
+        // geometry of each scanned pass rebuilt from an opaque lane index
+        // instead of eight per-pass VGPRs kept across the redraw loop
+        (void)cl;
+        const int ln = loop_lane(lane);
+#pragma unroll
+        for (int i = WS::NP - 1; i >= 0; i--) {
+            if (i * 64 > last || i < stop) continue;     // wave-uniform
+            const int p = i * 64 + ln;
+            const int pc = min(p, N1);
+            const int r = div_c(P, p), c = p - r * C;
+            const int x = col[pc];
+            const int u1 = col[max(pc - C, 0)], u2 = col[max(pc - 2 * C, 0)];
+            const int h1 = col[min(pc + 1, N1)], h2 = col[min(pc + 2, N1)];
+            const uint32_t tbad = ALL1 ? 0u : (uint32_t)((int)typ[pc] - 1) >> 31;
+            const uint32_t vbad = (p < N && r >= 2) ? 0u : 1u, hbad = (p < N && c + 2 < C) ? 0u : 1u;
+            const uint32_t vb = vbad | tbad | ne(u1, x) | ne(u2, x);
+            const uint32_t hb = hbad | tbad | ne(h1, x) | ne(h2, x);
+            const int base = (((r & 63) << 8) | (255 - (c & 255))) << 1;
+            best = max(best, max(vb == 0 ? base | 1 : -1, hb == 0 ? base : -1));
+            if (stop == -2 && __ballot(best >= 0) != 0ULL) stop = i - 1;
+        }
+    } else if constexpr (!ROLL || WS::NP <= 2) {
 #pragma unroll
         for (int i = WS::NP - 1; i >= 0; i--) {
             if (i * 64 > last || i < stop) continue;     // wave-uniform
@@ -1027,7 +1050,9 @@ __device__ __forceinline__ int ensure_playable(const Params &P, WS &w, int lane,
             WSYNC();
             lim = min(P.R - 1, max(row + 2, ra));
         }
-        if (scan_effective(P, w, lane, cl, (P.smask & SP_COOKIE) == 0)) break;
+        // generate_board's boards (ALL1: every type 1, no cookie) are line-free
+        // here, so the scan needs no precheck
+        if (scan_effective(P, w, lane, cl, ALL1 || (P.smask & SP_COOKIE) == 0)) break;
         if (shuffles >= TMG_MAX_SHUFFLES) return fl | FL_ERR;
         COVER(CV_SHUFFLE);
         WSYNC();

@@ -58,7 +58,7 @@ def _ptr(t: torch.Tensor):
 class TileMatchVecEnv:
     def __init__(self, num_envs: int, num_rows: int, num_cols: int, num_colours: int, num_moves: int,
                  colourless_specials=(), colour_specials=(), seed: int = 0, seeds=None, device=None,
-                 autoreset: bool = True, groups: int = 1):
+                 autoreset: bool = True, groups: int = 1, lib_path: str = None):
         if device is None:
             device = torch.device("cuda", torch.cuda.current_device())
         device = torch.device(device)
@@ -71,8 +71,9 @@ class TileMatchVecEnv:
         self.colour_specials = list(colour_specials)
         self.specials_mask = _native.specials_mask(colourless_specials, colour_specials)
         self.autoreset = bool(autoreset)
+        # lib_path: another build of libtmg.so (a diagnostic variant) for this env's context
         self.ctx = _native.Context(device.index if device.index is not None else torch.cuda.current_device(),
-                                   num_rows, num_cols, num_colours, self.specials_mask, num_moves)
+                                   num_rows, num_cols, num_colours, self.specials_mask, num_moves, lib_path=lib_path)
         self.num_actions = self.ctx.num_actions
         self.mask_words = self.ctx.mask_words
         N = self.num_envs
