@@ -65,3 +65,23 @@ def test_reset_with_seed_equals_ctor_seed():
     e2 = TileMatchEnv(6, 6, 4, 5, [], ["bomb"], seed=99)
     o2, i2 = e2.reset(seed=11)
     assert np.array_equal(o1["board"], o2["board"]) and i1 == i2
+
+
+@pytest.mark.gpu
+def test_is_move_effective_any_shape():
+    """The module-level is_move_effective and Board.possible_move(grid)
+    (board.py:558-569, 735-787) accept boards of any shape, including ones no
+    generated board could take (2x2, 1xC, 2xC): they run on a cached scan-only
+    context (tmg_create_scan), against the oracle's mask."""
+    from oracle import oracle as orc
+    from tile_match_gym_amd.tile_match_env import Board, action_to_coords, is_move_effective
+    rs = np.random.default_rng(8)
+    for R, C in ((2, 2), (1, 3), (1, 5), (2, 3), (3, 2), (2, 5), (3, 3), (4, 4)):
+        for _ in range(6):
+            b = np.stack([rs.integers(1, 3, (R, C)), rs.choice([1, 1, 1, 2, 3, 4, -1], (R, C))]).astype(np.int32)
+            b[0][b[1] == -1] = 0
+            want, any_ = orc.effective_mask(b.astype(np.int8))
+            got = np.array([is_move_effective(b, c1, c2) for c1, c2 in action_to_coords(R, C)])
+            assert np.array_equal(got, want), (R, C, b)
+            bd = Board(R, C, 3, [], [], board=b)
+            assert bd.possible_move() == any_ and bd.possible_move(b) == any_

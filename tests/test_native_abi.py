@@ -88,7 +88,8 @@ def test_viability_matches_state_counts():
                     continue
                 playable, _ = orc.count_states(R, C, k)
                 assert _native.viable(R, C, k) == (playable > 0), (R, C, k, playable)
-    for shape in ((10, 10, 4), (20, 20, 6), (8, 8, 3), (1, 13, 2), (2, 64, 2), (64, 8, 15)):
+    for shape in ((10, 10, 4), (20, 20, 6), (8, 8, 3), (1, 13, 2), (2, 64, 2), (64, 8, 15),
+                  (16, 16, 2), (20, 20, 2), (12, 30, 2), (64, 8, 2)):     # 2 colours: found by backtracking
         assert _native.viable(*shape), shape
 
 

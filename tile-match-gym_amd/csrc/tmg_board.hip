@@ -87,15 +87,11 @@ namespace tmg {
 enum : int { SP_COOKIE = 1, SP_VLASER = 2, SP_HLASER = 4, SP_BOMB = 8 };
 enum : int { M_NORMAL = 0, M_VLASER = 1, M_HLASER = 2, M_BOMB = 3, M_COOKIE = 4 };
 enum : int { FL_DONE = 1, FL_COMBO = 2, FL_SHUF = 4, FL_RESET = 8, FL_OVF = 0x40, FL_ERR = 0x80 };
-// internal (never stored): the step needs the lane-0 list machinery
-enum : int { FL_LISTS = 0x100 };
-// The general step runs in tiers (step_env's TIER): the main step kernel
-// carries only the wave-parallel cascade forms; a step that needs the lane-0
-// list machinery (process_colour_lines' rarer cases, cookie / DFS
-// activation, combination_match) is queued, unwritten, for list_kernel,
-// which re-runs it with LDS lists; a step that outgrows those is queued for
-// spill_kernel, which re-runs it on worst-case global-memory lists.
-enum : int { TIER_MAIN = 0, TIER_LIST = 1, TIER_SPILL = 2 };
+// The general step runs in two tiers (step_env's TIER): the step kernel with
+// its lane-0 lists in LDS (WsSerial), and, for the steps whose cascade
+// outgrows those, spill_kernel, which re-runs them on worst-case
+// global-memory lists (WsSerialBig).
+enum : int { TIER_MAIN = 0, TIER_SPILL = 2 };
 // sticky status (tmg_status): what any env met since the last clear
 enum : uint32_t { ST_INTERNAL = 1, ST_OVERFLOW = 2, ST_CALLER = 4 };
 
@@ -113,9 +109,6 @@ enum : uint32_t { ST_INTERNAL = 1, ST_OVERFLOW = 2, ST_CALLER = 4 };
 // Per-stream queue of the envs whose step ran out of LDS list space
 // (step_env), drained by spill_kernel.  Sized by the host for the envs of
 // the launch (cap >= n), so every such env fits: no step is ever dropped.
-#ifndef TMG_LIST_WAVES
-#define TMG_LIST_WAVES 2048      // list_kernel workgroups at most (one wave each; spare ones exit at once)
-#endif
 #ifndef TMG_SPILL_WAVES
 #define TMG_SPILL_WAVES 32       // spill_kernel workgroups (one wave, one WsSerialBig each)
 #endif
@@ -153,8 +146,6 @@ enum : int {
     CV_SHUFFLE,          // shuffle in the ensure-playable loop
     CV_REJECT,           // Lemire rejection: serial replay of a draw batch
     CV_FAST,             // fast_clear step (general kernel, no specials enabled)
-    CV_LIST,             // step queued for list_kernel (needs the lane-0 machinery)
-    CV_LIST_RUN,         // step re-run by list_kernel
     CV_COUNT = 32
 };
 #if TMG_COVER
@@ -189,7 +180,6 @@ struct Params {
     int oh_dtype, oh_ch, oh_nsel; // TMG_DTYPE_*; channels = k + nsel
     uint32_t oh_sel;              // type ids of the special channels, int8 each (wrappers.py:37-46)
     SpillQ *spill;                // this launch's stream's spill queue (general kernels)
-    SpillQ *listq;                // this launch's stream's list-tier queue (general kernels)
     void *spill_ws;               // TMG_SPILL_WAVES WsSerialBig<MAXN> for spill_kernel
     unsigned long long *cover;    // TMG_COVER builds: CV_COUNT hit counters (null otherwise)
     uint64_t *stamps;             // TMG_STAMPS builds: per-env phase stamps (null otherwise)
@@ -223,7 +213,6 @@ inline Params make_params(int R, int C, int k, int smask, int num_moves, const u
     P.sb_rows = nullptr;
     P.status = nullptr;
     P.spill = nullptr;
-    P.listq = nullptr;
     P.spill_ws = nullptr;
     P.cover = nullptr;
     P.stamps = nullptr;
@@ -1074,9 +1063,8 @@ __device__ __forceinline__ int generate_board(const Params &P, WS &w, int lane, 
     return ensure_playable<ROLL, PRE, true>(P, w, lane, J, g, cl) & FL_ERR;         // types all 1
 }
 
-// Queue env e for list_kernel / spill_kernel.  The host sizes each queue for
-// every env of the launch, so this cannot fail; false only if that sizing
-// were broken.
+// Queue env e for spill_kernel.  The host sizes the queue for every env of
+// the launch, so this cannot fail; false only if that sizing were broken.
 __device__ __forceinline__ bool queue_env(SpillQ *q, int lane, int64_t e) {
     int ok = 0;
     if (lane == 0) {
@@ -1760,14 +1748,10 @@ struct Serial {
 // board in w.effw.
 // clean: the board held no line before the swap (it came out of this file's
 // ensure-playable loop), which bounds the first line search.
-// TIER (general kernels): TIER_MAIN has no lane-0 list machinery — a step
-// that needs it returns at once with FL_LISTS (nothing of it is kept: the
-// caller queues the env for list_kernel).
 template <int MAXN, bool GEN, int SBNB, bool CODD, int TIER, class WS, class L>
 __device__ __forceinline__ int board_move(const Params &P, WS &w, int lane, const LaneJump &J, Rng &g,
                           const Cells<MAXN / 64> &cl_unused, int p1, int p2, int &flags, int &nn, int &na, int64_t e,
                           L *lists, bool clean) {
-    constexpr bool LISTS = GEN && TIER != TIER_MAIN;
     (void)cl_unused;
     // the per-lane cell coordinates are rebuilt where they are used (a few
     // VALU ops) rather than kept live across the cascade loop
@@ -1791,10 +1775,7 @@ __device__ __forceinline__ int board_move(const Params &P, WS &w, int lane, cons
     bool ovf = false, err = false;
     if (((t1 != 0 && t1 != 1) && (t2 != 0 && t2 != 1)) || t1 < 0 || t2 < 0) {   // :357-364
         flags |= FL_COMBO;
-        if constexpr (GEN && !LISTS) {
-            flags |= FL_LISTS;                                              // combination_match: list tier
-            return 0;
-        } else if constexpr (GEN) {
+        if constexpr (GEN) {
             COVER(CV_COMBO);
             int nz = count_colour_nonzero(P, w, lane);
             if (lane == 0) {
@@ -1835,7 +1816,6 @@ __device__ __forceinline__ int board_move(const Params &P, WS &w, int lane, cons
                 if (r < 0) break;
                 if (r > 0) { elim += r; iters++; lim = P.R - 1; continue; }
                 COVER(CV_SB_FALLBACK);
-                if constexpr (!LISTS) { flags |= FL_LISTS; return 0; }
             }
         }
         Det<MAXN / 64> d;
@@ -1862,10 +1842,7 @@ __device__ __forceinline__ int board_move(const Params &P, WS &w, int lane, cons
                 }
                 if (plain) COVER(CV_LDS_FALLBACK);
             }
-            if constexpr (GEN && !LISTS) {
-                flags |= FL_LISTS;
-                return 0;
-            } else if constexpr (GEN) {
+            if constexpr (GEN) {
                 int nz = count_colour_nonzero(P, w, lane);
                 COVER(CV_SERIAL_STEP);
                 if (lane == 0) {
@@ -1928,7 +1905,7 @@ __device__ __forceinline__ void store_rng(uint64_t *p, const Rng &g, int lane) {
 // launch masked by FL_RESET (the 512-cell kernels: the reset kernel's
 // occupancy is far higher than the general step kernel's).  Returns the ST_*
 // bits this step raises for the sticky status word.
-template <int MAXN, bool GEN, int SBNB, bool CODD, int TIER = TIER_MAIN, class WS = Ws<MAXN, false>,
+template <int MAXN, bool GEN, int SBNB, bool CODD, int TIER = TIER_MAIN, class WS = Ws<MAXN, GEN>,
           class L = WsSerial<MAXN>>
 __device__ __forceinline__ uint32_t step_env(
     const Params &P, WS &w, int lane, int64_t e, int8_t *__restrict__ board, uint64_t *__restrict__ rng, int32_t *__restrict__ timer,
@@ -1976,7 +1953,7 @@ __device__ __forceinline__ uint32_t step_env(
     if constexpr (GEN) {
         for (int p = lane; p < N; p += 64) w.mark[p] = 0;
     }
-    if constexpr (TIER != TIER_MAIN) COVER(TIER == TIER_LIST ? CV_LIST_RUN : CV_SPILL_RUN);
+    if constexpr (TIER == TIER_SPILL) COVER(CV_SPILL_RUN);
     WSYNC();
     if constexpr (!GEN) {                                                   // lean variant precondition
         bool ok = true;
@@ -2001,15 +1978,7 @@ __device__ __forceinline__ uint32_t step_env(
         else elim = board_move<MAXN, GEN, SBNB, CODD, TIER>(P, w, lane, J, g, cl, p1, p2, flags, nn, na, e, lists,
                                                              trust_eff != 0);
         changed = true;
-        if constexpr (GEN && TIER == TIER_MAIN) {
-            // the step needs the lane-0 list machinery: nothing of this env
-            // has been written; list_kernel re-runs the whole step
-            if (flags & FL_LISTS) {
-                if (queue_env(P.listq, lane, e)) { COVER(CV_LIST); return 0; }
-                flags = (flags & ~FL_LISTS) | FL_ERR;                        // unreachable (queue sized for n)
-            }
-        }
-        if constexpr (GEN && TIER != TIER_MAIN) {
+        if constexpr (GEN) {
             if (flags & FL_OVF) {
                 // the LDS lists ran out: nothing of this env has been written;
                 // queue it for spill_kernel, which re-runs the whole step on
@@ -2017,7 +1986,7 @@ __device__ __forceinline__ uint32_t step_env(
                 // every env of the launch and WsSerialBig cannot run out, so the
                 // fall-through is unreachable; were it reached, the step is
                 // flagged as an internal error, never written back as exact.
-                if constexpr (TIER == TIER_LIST) {
+                if constexpr (TIER == TIER_MAIN) {
                     if (queue_env(P.spill, lane, e)) { COVER(CV_SPILL); return 0; }
                 }
                 flags = (flags & ~FL_OVF) | FL_ERR;
@@ -2073,52 +2042,17 @@ __global__ __launch_bounds__(64 * TMG_WPB, MAXN == 128 ? (GEN ? TMG_GEN128_WAVES
     int32_t *__restrict__ n_act, uint8_t *__restrict__ flags_out, uint64_t *__restrict__ eff, int trust_eff,
     int autoreset) {
     TMG_SMEM_DECL(smem);
-    using WS = Ws<MAXN, false>;                   // the main tier keeps no lane-0 lists
+    using WS = Ws<MAXN, GEN>;
     const int lane = threadIdx.x & 63;
     const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
     WS &w = reinterpret_cast<WS *>(smem)[wv];
     const int64_t e = wg_env0() + wv;
     if (e >= n) return;
+    WsSerial<MAXN> *lists = nullptr;
+    if constexpr (GEN) lists = &w.s;
     const uint32_t st = step_env<MAXN, GEN, SBNB, CODD, TIER_MAIN, WS, WsSerial<MAXN>>(
-        P, w, lane, e, board, rng, timer, actions, reward, n_new, n_act, flags_out, eff, trust_eff, autoreset, nullptr);
+        P, w, lane, e, board, rng, timer, actions, reward, n_new, n_act, flags_out, eff, trust_eff, autoreset, lists);
     note_status(P, lane, st);
-}
-
-// Re-runs the steps the general step kernel queued for the lane-0 list
-// machinery (FL_LISTS: TIER_MAIN), with LDS lists (WsSerial): launched right
-// after every general step launch on the same stream with the same buffers,
-// a grid of one-wave workgroups taking queue entries blockIdx.x,
-// blockIdx.x + gridDim.x, ...  An empty queue costs one load per wave.
-// Steps whose lists run out go on to spill_kernel.
-template <int MAXN, int SBNB = 0, bool CODD = false>
-__global__ __launch_bounds__(64, MAXN == 128 ? TMG_GEN128_WAVES : TMG_GEN512_WAVES) void list_kernel(
-    Params P, int64_t n, int8_t *__restrict__ board, uint64_t *__restrict__ rng, int32_t *__restrict__ timer,
-    const int32_t *__restrict__ actions, int32_t *__restrict__ reward, int32_t *__restrict__ n_new,
-    int32_t *__restrict__ n_act, uint8_t *__restrict__ flags_out, uint64_t *__restrict__ eff, int trust_eff,
-    int autoreset) {
-    TMG_SMEM_DECL(smem);
-    using WS = Ws<MAXN, true>;
-    const int lane = threadIdx.x & 63;
-    WS &w = *reinterpret_cast<WS *>(smem);
-    SpillQ *q = P.listq;
-    const int64_t queued = (int64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)q->count);
-    const int cnt = (int)(queued < q->cap ? queued : q->cap);
-    int done = 0;
-    for (int i = (int)blockIdx.x; i < cnt; i += (int)gridDim.x) {
-        const int64_t e = (int64_t)bcast64((uint64_t)q->env[i]);
-        if (e < 0 || e >= n) continue;
-        WSYNC();
-        const uint32_t st = step_env<MAXN, true, SBNB, CODD, TIER_LIST, WS, WsSerial<MAXN>>(
-            P, w, lane, e, board, rng, timer, actions, reward, n_new, n_act, flags_out, eff, trust_eff, autoreset,
-            &w.s);
-        note_status(P, lane, st);
-        done++;
-    }
-    if (lane == 0) {
-        if (done) atomicAdd(&q->total, (unsigned long long)done);
-        __threadfence();
-        if (atomicAdd(&q->done, 1u) == gridDim.x - 1) { q->count = 0u; q->done = 0u; }   // the last wave empties the queue
-    }
 }
 
 // Re-runs the steps the general step kernel queued on running out of LDS list

@@ -49,14 +49,12 @@ struct tmg_ctx {
     int maxn;
     int sb;              // scalar-bitboard kernels (<= 128 cells, C <= 63)
     int scan_only;       // tmg_create_scan: tmg_effective / tmg_onehot only
-    // list-tier and spill queues of the general kernels, one pair per stream
-    // the context steps on (a queue is only ever touched by the launches of
-    // its own stream, in order), each holding at least as many entries as the
-    // largest launch on it
+    // spill queue of the general kernels, one per stream the context steps on
+    // (a queue is only ever touched by the launches of its own stream, in
+    // order), holding at least as many entries as the largest launch on it
     struct Spill {
         hipStream_t stream;
-        tmg::SpillQ *q;       // spill_kernel's queue
-        tmg::SpillQ *lq;      // list_kernel's queue
+        tmg::SpillQ *q;
         int64_t cap;
         void *ws;
     };
@@ -93,40 +91,36 @@ static int new_queue(hipStream_t s, int64_t cap, unsigned long long total, tmg::
     return rc;
 }
 
-// The stream's list-tier and spill queues, holding at least n entries each
-// (zeroed on s).  Growing waits for s first: the old queues may still be read
-// by a queued launch.
-static int spill_for(tmg_ctx *ctx, hipStream_t s, int64_t n, tmg::SpillQ **q, tmg::SpillQ **lq, void **ws) {
+// The stream's spill queue, holding at least n entries (zeroed on s).
+// Growing waits for s first: the old queue may still be read by a queued
+// launch.
+static int spill_for(tmg_ctx *ctx, hipStream_t s, int64_t n, tmg::SpillQ **q, void **ws) {
     std::lock_guard<std::mutex> lock(ctx->mu);
     tmg_ctx::Spill *sp = nullptr;
     for (auto &x : ctx->spills)
         if (x.stream == s) sp = &x;
     if (!sp) {
-        ctx->spills.push_back(tmg_ctx::Spill{s, nullptr, nullptr, 0, nullptr});
+        ctx->spills.push_back(tmg_ctx::Spill{s, nullptr, 0, nullptr});
         sp = &ctx->spills.back();
         int rc = hip_check(hipMalloc(&sp->ws, tmg::spill_ws_bytes(ctx->maxn) * TMG_SPILL_WAVES), "hipMalloc");
         if (rc) { ctx->spills.pop_back(); return rc; }
     }
     if (sp->cap < n) {
         int rc = 0;
-        unsigned long long total = 0, ltotal = 0;
+        unsigned long long total = 0;
         if (sp->q) {
             rc = hip_check(hipStreamSynchronize(s), "hipStreamSynchronize");
             if (!rc) rc = hip_check(hipMemcpy(&total, &sp->q->total, sizeof total, hipMemcpyDeviceToHost), "hipMemcpy");
-            if (!rc) rc = hip_check(hipMemcpy(&ltotal, &sp->lq->total, sizeof ltotal, hipMemcpyDeviceToHost), "hipMemcpy");
             (void)hipFree(sp->q);
-            (void)hipFree(sp->lq);
-            sp->q = sp->lq = nullptr;
+            sp->q = nullptr;
             sp->cap = 0;
         }
         const int64_t cap = n < 64 ? 64 : n;
         if (!rc) rc = new_queue(s, cap, total, &sp->q);
-        if (!rc) rc = new_queue(s, cap, ltotal, &sp->lq);
         if (rc) return rc;
         sp->cap = cap;
     }
     *q = sp->q;
-    *lq = sp->lq;
     *ws = sp->ws;
     return 0;
 }
@@ -156,7 +150,7 @@ static int do_step(tmg_ctx *ctx, Params P, StepArgs a, hipStream_t s) {
     // masked by FL_RESET, which runs at several times their occupancy
     const int deferred = a.autoreset && (ctx->maxn == 512 || !lean || TMG_LEAN_DEFER);
     if (!lean) {
-        int rc = spill_for(ctx, s, a.n, &P.spill, &P.listq, &P.spill_ws);
+        int rc = spill_for(ctx, s, a.n, &P.spill, &P.spill_ws);
         if (rc) return rc;
     }
     if (deferred) a.autoreset = 2;
@@ -169,17 +163,9 @@ static int do_step(tmg_ctx *ctx, Params P, StepArgs a, hipStream_t s) {
     }
     int rc = hip_check(hipGetLastError(), "kernel launch");
     if (rc) return rc;
-    if (!lean) {
-        // re-run the steps that need the lane-0 list machinery (list tier),
-        // then those that ran out of LDS list space (spill tier)
-        if (ctx->maxn == 128) {
-            if (ctx->sb && (P.C & 1)) tmg::launch_list128_odd(s, P, a);
-            else tmg::launch_list128_even(ctx->sb, s, P, a);
-            tmg::launch_spill128(s, P, a);
-        } else {
-            tmg::launch_list512(s, P, a);
-            tmg::launch_spill512(s, P, a);
-        }
+    if (!lean) {                                   // re-run the steps that ran out of LDS list space
+        if (ctx->maxn == 128) tmg::launch_spill128(s, P, a);
+        else tmg::launch_spill512(s, P, a);
         rc = hip_check(hipGetLastError(), "kernel launch");
         if (rc) return rc;
     }
@@ -332,7 +318,6 @@ void free_ctx(tmg_ctx *c) {
     if (c->d_stamps) (void)hipFree(c->d_stamps);
     for (const auto &x : c->spills) {
         if (x.q) (void)hipFree(x.q);
-        if (x.lq) (void)hipFree(x.lq);
         if (x.ws) (void)hipFree(x.ws);
     }
     delete c;

@@ -1,5 +1,5 @@
 // tmg_kernels.hip — kernel instantiations and their host launchers
-// (tmg_launch.h).  Compiled once per translation unit, TMG_TU = 1..9, so the
+// (tmg_launch.h).  Compiled once per translation unit, TMG_TU = 1..7, so the
 // heavy template instantiations build in parallel; each TU registers only its
 // own kernels.
 #include <hip/hip_runtime.h>
@@ -11,7 +11,7 @@
 #endif
 
 #ifndef TMG_TU
-#error "compile tmg_kernels.hip with -DTMG_TU=1..9"
+#error "compile tmg_kernels.hip with -DTMG_TU=1..7"
 #endif
 
 namespace tmg {
@@ -20,7 +20,7 @@ namespace {
 
 template <int MAXN, bool GEN, int NB, bool CODD>
 void step_one(dim3 grid, hipStream_t s, const Params &P, const StepArgs &a) {
-    const size_t lds = sizeof(Ws<MAXN, false>) * TMG_WPB;          // no lane-0 lists in the main tier
+    const size_t lds = sizeof(Ws<MAXN, GEN>) * TMG_WPB;
     hipLaunchKernelGGL((step_kernel<MAXN, GEN, NB, CODD>), grid, dim3(64 * TMG_WPB), lds, s, P, a.n, a.board, a.rng,
                        a.timer, a.actions, a.reward, a.n_new, a.n_act, a.flags, a.eff, a.trust_eff, a.autoreset);
 }
@@ -33,25 +33,6 @@ void step_sb(dim3 grid, hipStream_t s, const Params &P, const StepArgs &a) {
     case 2: step_one<128, GEN, 2, CODD>(grid, s, P, a); break;
     case 3: step_one<128, GEN, 3, CODD>(grid, s, P, a); break;
     default: step_one<128, GEN, 4, CODD>(grid, s, P, a); break;
-    }
-}
-
-// the list tier: min(n, TMG_LIST_WAVES) one-wave workgroups drain the queue
-template <int MAXN, int NB, bool CODD>
-void list_one(hipStream_t s, const Params &P, const StepArgs &a) {
-    const size_t lds = sizeof(Ws<MAXN, true>);
-    const unsigned g = (unsigned)(a.n < TMG_LIST_WAVES ? a.n : TMG_LIST_WAVES);
-    hipLaunchKernelGGL((list_kernel<MAXN, NB, CODD>), dim3(g), dim3(64), lds, s, P, a.n, a.board, a.rng, a.timer,
-                       a.actions, a.reward, a.n_new, a.n_act, a.flags, a.eff, a.trust_eff, a.autoreset);
-}
-
-template <bool CODD>
-void list_sb(hipStream_t s, const Params &P, const StepArgs &a) {
-    switch (sb_planes(P.k)) {
-    case 1: list_one<128, 1, CODD>(s, P, a); break;
-    case 2: list_one<128, 2, CODD>(s, P, a); break;
-    case 3: list_one<128, 3, CODD>(s, P, a); break;
-    default: list_one<128, 4, CODD>(s, P, a); break;
     }
 }
 
@@ -93,6 +74,11 @@ void launch_step_gen128_even(bool sb, dim3 grid, hipStream_t s, const Params &P,
 }
 #endif
 
+#if TMG_TU == 7
+void launch_spill128(hipStream_t s, const Params &P, const StepArgs &a) { spill_one<128>(s, P, a); }
+void launch_spill512(hipStream_t s, const Params &P, const StepArgs &a) { spill_one<512>(s, P, a); }
+#endif
+
 #if TMG_TU == 3
 void launch_step_gen128_odd(dim3 grid, hipStream_t s, const Params &P, const StepArgs &a) {
     step_sb<true, true>(grid, s, P, a);
@@ -112,23 +98,6 @@ void launch_reset512(dim3 grid, hipStream_t s, const Params &P, int64_t n, int8_
 void launch_effective512(dim3 grid, hipStream_t s, const Params &P, int64_t n, const int8_t *board, uint64_t *eff) {
     effective_one<512>(grid, s, P, n, board, eff);
 }
-#endif
-
-#if TMG_TU == 7
-void launch_list128_even(bool sb, hipStream_t s, const Params &P, const StepArgs &a) {
-    if (sb) list_sb<false>(s, P, a);
-    else list_one<128, 0, false>(s, P, a);
-}
-void launch_spill128(hipStream_t s, const Params &P, const StepArgs &a) { spill_one<128>(s, P, a); }
-#endif
-
-#if TMG_TU == 8
-void launch_list128_odd(hipStream_t s, const Params &P, const StepArgs &a) { list_sb<true>(s, P, a); }
-#endif
-
-#if TMG_TU == 9
-void launch_list512(hipStream_t s, const Params &P, const StepArgs &a) { list_one<512, 0, false>(s, P, a); }
-void launch_spill512(hipStream_t s, const Params &P, const StepArgs &a) { spill_one<512>(s, P, a); }
 #endif
 
 #if TMG_TU == 5

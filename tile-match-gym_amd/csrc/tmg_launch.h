@@ -29,18 +29,14 @@ dim3 env_grid(int64_t n);
 // TU 1 — lean step kernels (no specials, cached mask trusted), <= 128 cells;
 // sb: scalar-bitboard variants (C <= 63)
 void launch_step_lean128(bool sb, dim3 grid, hipStream_t s, const Params &P, const StepArgs &a);
-// TU 2 / 3 — general <= 128-cell step kernels (main tier), C even / odd (the
+// TU 2 / 3 — general <= 128-cell step kernels, C even / odd (the
 // non-bitboard one lives in TU 2)
 void launch_step_gen128_even(bool sb, dim3 grid, hipStream_t s, const Params &P, const StepArgs &a);
 void launch_step_gen128_odd(dim3 grid, hipStream_t s, const Params &P, const StepArgs &a);
-// TU 7 / 8 — their list tier (C even + the non-bitboard one / C odd), and the
-// 128-cell spill kernel (TU 7)
-void launch_list128_even(bool sb, hipStream_t s, const Params &P, const StepArgs &a);
-void launch_list128_odd(hipStream_t s, const Params &P, const StepArgs &a);
-void launch_spill128(hipStream_t s, const Params &P, const StepArgs &a);
-// TU 4 — 512-cell kernels; TU 9 — their list and spill tiers
+// TU 4 — 512-cell kernels
 void launch_step512(bool gen, dim3 grid, hipStream_t s, const Params &P, const StepArgs &a);
-void launch_list512(hipStream_t s, const Params &P, const StepArgs &a);
+// TU 7 — the spill tier (steps whose cascade outgrew the LDS lists)
+void launch_spill128(hipStream_t s, const Params &P, const StepArgs &a);
 void launch_spill512(hipStream_t s, const Params &P, const StepArgs &a);
 void launch_reset512(dim3 grid, hipStream_t s, const Params &P, int64_t n, int8_t *board, uint64_t *rng,
                      int32_t *timer, uint64_t *eff, const uint8_t *env_mask, int mask_bits);

@@ -203,7 +203,7 @@ static void run_blocks(int64_t n, size_t lds, F kernel) {
 
 static uint64_t g_sbrows[64 * 4];
 static uint32_t g_status[4];
-static std::vector<int64_t> g_spill_buf, g_list_buf;   // SpillQs with room for every env of the call
+static std::vector<int64_t> g_spill_buf;          // a SpillQ with room for every env of the call
 static unsigned long long g_spill_total = 0;
 static unsigned long long g_cover[tmg::CV_COUNT];
 static std::vector<unsigned char> g_spill_ws(sizeof(tmg::WsSerialBig<512>) * TMG_SPILL_WAVES);
@@ -245,24 +245,7 @@ struct EmuStep {
 template <int MAXN, bool GEN, int NB, bool CODD>
 static void emu_step_kernel(EmuStep &S) {
     const tmg::Params &P = *S.P;
-    run_blocks(S.n, sizeof(tmg::Ws<MAXN, false>), [&] { tmg::step_kernel<MAXN, GEN, NB, CODD>(P, S.n, S.board, S.rng, S.timer, S.actions, S.reward, S.n_new, S.n_act, S.flags, S.eff, S.trust_eff, S.autoreset); });
-}
-
-// list_kernel after a general step launch, as tmg_capi.hip's do_step
-template <int MAXN, int NB, bool CODD>
-static void emu_list(EmuStep &S) {
-    const tmg::Params &P = *S.P;
-    const int64_t g = S.n < 8 ? S.n : 8;
-    run_grid(g, sizeof(tmg::Ws<MAXN, true>), [&] { tmg::list_kernel<MAXN, NB, CODD>(P, S.n, S.board, S.rng, S.timer, S.actions, S.reward, S.n_new, S.n_act, S.flags, S.eff, S.trust_eff, S.autoreset); });
-}
-template <bool CODD>
-static void emu_list_sb(EmuStep &S) {
-    switch (tmg::sb_planes(S.P->k)) {
-    case 1: emu_list<128, 1, CODD>(S); break;
-    case 2: emu_list<128, 2, CODD>(S); break;
-    case 3: emu_list<128, 3, CODD>(S); break;
-    default: emu_list<128, 4, CODD>(S); break;
-    }
+    run_blocks(S.n, sizeof(tmg::Ws<MAXN, GEN>), [&] { tmg::step_kernel<MAXN, GEN, NB, CODD>(P, S.n, S.board, S.rng, S.timer, S.actions, S.reward, S.n_new, S.n_act, S.flags, S.eff, S.trust_eff, S.autoreset); });
 }
 
 // spill_kernel after a general step launch, as tmg_capi.hip's do_step
@@ -319,7 +302,6 @@ int emu_step(int R, int C, int k, int smask, int moves, int64_t n, int8_t *board
     if (!g_jump_init) { tmg::build_jump_table(g_jump); g_jump_init = true; }
     tmg::Params P = make_params(R, C, k, smask, moves, g_jump);
     P.spill = spill_queue(g_spill_buf, n);
-    P.listq = spill_queue(g_list_buf, n);
     EmuStep S;
     S.P = &P; S.n = n; S.board = board; S.rng = rng; S.timer = timer; S.actions = actions; S.reward = reward;
     S.n_new = n_new; S.n_act = n_act; S.flags = flags; S.eff = eff; S.trust_eff = trust_eff; S.autoreset = autoreset;
@@ -335,16 +317,15 @@ int emu_step(int R, int C, int k, int smask, int moves, int64_t n, int8_t *board
             else if (P.C & 1) emu_step_sb<false, true>(S);
             else emu_step_sb<false, false>(S);
         } else {
-            if (!sb_ok(P)) { emu_step_kernel<128, true, 0, false>(S); emu_list<128, 0, false>(S); }
-            else if (P.C & 1) { emu_step_sb<true, true>(S); emu_list_sb<true>(S); }
-            else { emu_step_sb<true, false>(S); emu_list_sb<false>(S); }
+            if (!sb_ok(P)) emu_step_kernel<128, true, 0, false>(S);
+            else if (P.C & 1) emu_step_sb<true, true>(S);
+            else emu_step_sb<true, false>(S);
             emu_spill<128>(S);
         }
     } else if (lean) {
         emu_step_kernel<512, false, 0, false>(S);
     } else {
         emu_step_kernel<512, true, 0, false>(S);
-        emu_list<512, 0, false>(S);
         emu_spill<512>(S);
     }
     g_spill_total += P.spill->total;
