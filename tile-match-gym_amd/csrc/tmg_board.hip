@@ -110,7 +110,7 @@ enum : uint32_t { ST_INTERNAL = 1, ST_OVERFLOW = 2, ST_CALLER = 4 };
 // (step_env), drained by spill_kernel.  Sized by the host for the envs of
 // the launch (cap >= n), so every such env fits: no step is ever dropped.
 #ifndef TMG_SPILL_WAVES
-#define TMG_SPILL_WAVES 32       // spill_kernel workgroups (one wave, one WsSerialBig each)
+#define TMG_SPILL_WAVES 16       // spill_kernel workgroups (one wave, one WsSerialBig each)
 #endif
 struct SpillQ {
     uint32_t count, done;        // queued envs; spill_kernel waves finished
@@ -2061,14 +2061,22 @@ __global__ __launch_bounds__(64 * TMG_WPB, MAXN == 128 ? (GEN ? TMG_GEN128_WAVES
 // stream with the same buffers, TMG_SPILL_WAVES one-wave workgroups, each
 // with its own WsSerialBig.  An empty queue costs one load per wave.  The
 // generic (non-bitboard) path: bit-identical results by construction.
+// Small footprint on purpose (no LDS lists, at most TMG_SPILL_VGPR_WAVES'
+// worth of VGPRs, spilling to scratch instead): the launch follows every
+// general step on its stream and must find room on a chip busy with the
+// other streams' kernels at once, or it holds its stream back; the rare
+// steps it re-runs may go slowly.
+#ifndef TMG_SPILL_VGPR_WAVES
+#define TMG_SPILL_VGPR_WAVES 8
+#endif
 template <int MAXN>
-__global__ __launch_bounds__(64) void spill_kernel(
+__global__ __launch_bounds__(64, TMG_SPILL_VGPR_WAVES) void spill_kernel(
     Params P, int64_t n, int8_t *__restrict__ board, uint64_t *__restrict__ rng, int32_t *__restrict__ timer,
     const int32_t *__restrict__ actions, int32_t *__restrict__ reward, int32_t *__restrict__ n_new,
     int32_t *__restrict__ n_act, uint8_t *__restrict__ flags_out, uint64_t *__restrict__ eff, int trust_eff,
     int autoreset) {
     TMG_SMEM_DECL(smem);
-    using WS = Ws<MAXN, true>;
+    using WS = Ws<MAXN, false>;                   // the lists are global (WsSerialBig)
     const int lane = threadIdx.x & 63;
     WS &w = *reinterpret_cast<WS *>(smem);
     SpillQ *q = P.spill;

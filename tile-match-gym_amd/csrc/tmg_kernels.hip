@@ -38,7 +38,7 @@ void step_sb(dim3 grid, hipStream_t s, const Params &P, const StepArgs &a) {
 
 template <int MAXN>
 void spill_one(hipStream_t s, const Params &P, const StepArgs &a) {
-    const size_t lds = sizeof(Ws<MAXN, true>);
+    const size_t lds = sizeof(Ws<MAXN, false>);
     hipLaunchKernelGGL((spill_kernel<MAXN>), dim3(TMG_SPILL_WAVES), dim3(64), lds, s, P, a.n, a.board, a.rng, a.timer,
                        a.actions, a.reward, a.n_new, a.n_act, a.flags, a.eff, a.trust_eff, a.autoreset);
 }

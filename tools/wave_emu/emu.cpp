@@ -252,7 +252,7 @@ static void emu_step_kernel(EmuStep &S) {
 template <int MAXN>
 static void emu_spill(EmuStep &S) {
     const tmg::Params &P = *S.P;
-    run_grid(TMG_SPILL_WAVES, sizeof(tmg::Ws<MAXN, true>), [&] { tmg::spill_kernel<MAXN>(P, S.n, S.board, S.rng, S.timer, S.actions, S.reward, S.n_new, S.n_act, S.flags, S.eff, S.trust_eff, S.autoreset); });
+    run_grid(TMG_SPILL_WAVES, sizeof(tmg::Ws<MAXN, false>), [&] { tmg::spill_kernel<MAXN>(P, S.n, S.board, S.rng, S.timer, S.actions, S.reward, S.n_new, S.n_act, S.flags, S.eff, S.trust_eff, S.autoreset); });
 }
 
 template <bool GEN, bool CODD>
