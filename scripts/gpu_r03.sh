@@ -40,7 +40,7 @@ all)
   STAGE=tests bash scripts/gpu_r03.sh && STAGE=deep bash scripts/gpu_r03.sh && STAGE=bench bash scripts/gpu_r03.sh
   ;;
 prof)
-  for c in c2 c3 c5; do
+  for c in ${CONFIGS:-c2 c3 c5}; do
     timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $OUT/prof_$c -o run --output-format csv -- \
       python3 bench.py --config $c --steps 90 --warmup 30 --no-cpu-baseline > $OUT/${c}_prof_bench.log 2>&1 \
       || { echo "prof $c failed"; tail $OUT/${c}_prof_bench.log; exit 1; }

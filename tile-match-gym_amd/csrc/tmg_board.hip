@@ -71,6 +71,16 @@ namespace tmg {
 #ifndef TMG_RQ128_WAVES
 #define TMG_RQ128_WAVES 5      // min waves per SIMD for the 128-cell reset-queue kernel (87 VGPRs, no spill)
 #endif
+#ifndef TMG_RESET_RECOMP
+// 512-cell reset kernel: 1 rebuilds the line search's cell geometry per pass
+// (79 VGPRs, no scratch, 6 waves/SIMD) instead of keeping it in VGPRs (96,
+// 88 B of scratch spills, 5 waves/SIMD); the rebuild's ~30 VALU per redraw
+// cost c5 10 % (1.04 vs 1.15 x 10^8): the kernel is VALU-bound
+#define TMG_RESET_RECOMP 0
+#endif
+#ifndef TMG_CELLS_ONCE
+#define TMG_CELLS_ONCE 1       // 512-cell board_move: cell geometry computed once per step (1) or rebuilt where used (0; c5 neutral)
+#endif
 #ifndef TMG_RESET512_WAVES
 #define TMG_RESET512_WAVES 5   // min waves per SIMD for the 512-cell reset kernel (caps its VGPRs; A/B 4 / 6 slower)
 #endif
@@ -424,7 +434,17 @@ __device__ __forceinline__ void rng_bcast(Rng &g) {
 
 struct LaneJump {
     U128 Aj, Gj, incG;    // A^{lane+1}, G_{lane+1}, G_{lane+1} * inc
+    // wave-uniform (512-cell kernels): A^64 and G_64 * inc, so a lane steps its
+    // own state one batch of 64 outputs further, s' = A^64 s + G_64 inc, with
+    // no cross-lane dependency (TMG_LANE_BATCH)
+    U128 A64, incG64;
 };
+#ifndef TMG_LANE_BATCH
+#define TMG_LANE_BATCH 1         // 512-cell reset kernel
+#endif
+#ifndef TMG_LANE_BATCH_STEP
+#define TMG_LANE_BATCH_STEP 0    // 512-cell step kernels (+5 VGPRs: 3 -> 2 waves/SIMD for the general one)
+#endif
 
 // single-lane stream (serial replays, shuffle)
 __device__ __forceinline__ uint64_t r_next64(Rng &g) {
@@ -486,12 +506,15 @@ __device__ __forceinline__ void draw_colours(const Params &P, int lane, const La
     const int n64 = (need + 1) >> 1;
     U128 s{g.slo, g.shi};
     uint64_t last_hi = 0;
+    U128 sj{0, 0};
+    uint64_t out = 0;
     for (int base = 0; base < n64; base += 64) {
-        U128 sj;
-        uint64_t out;
         if (pre && base == 0) {
             sj = pre->sj;
             out = pre->out;
+        } else if (!ONE && base > 0 && (J.A64.lo | J.A64.hi) != 0) {   // load_jump<.., LB>
+            sj = add128(mul128(sj, J.A64), J.incG64);               // the previous batch was a full 64
+            out = xsl_rr(sj);
         } else {
             sj = add128(mul128(J.Aj, s), J.incG);
             out = xsl_rr(sj);
@@ -504,10 +527,12 @@ __device__ __forceinline__ void draw_colours(const Params &P, int lane, const La
         *d0 = (T)(1 + (m0 >> 32));
         *d1 = (T)(1 + (m1 >> 32));
         rej |= (ok0 & ((uint32_t)m0 < P.thr)) | (ok1 & ((uint32_t)m1 < P.thr));
-        int cnt = n64 - base < 64 ? n64 - base : 64;
-        s.lo = rdlane64(sj.lo, cnt - 1);
-        s.hi = rdlane64(sj.hi, cnt - 1);
-        last_hi = rdlane64(out >> 32, cnt - 1);
+        const int cnt = n64 - base < 64 ? n64 - base : 64;
+        if (ONE || (J.A64.lo | J.A64.hi) == 0 || base + 64 >= n64) {   // the stream position after the batch
+            s.lo = rdlane64(sj.lo, cnt - 1);
+            s.hi = rdlane64(sj.hi, cnt - 1);
+            last_hi = rdlane64(out >> 32, cnt - 1);
+        }
         if constexpr (ONE) break;
     }
     if (P.thr != 0u && __ballot(rej) != 0ULL) {            // Lemire rejection: exact serial replay
@@ -842,7 +867,7 @@ __device__ __forceinline__ int first_line_row(const Params &P, const WS &w, int 
     const int8_t *col = w.brd, *typ = w.brd + N;
     const int last = min((lim + 1) * C, N) - 1;          // highest cell that may anchor a line
     int best = -1, stop = -2;                            // stop: lowest pass still to scan, once found
-    if constexpr (!ROLL && WS::NP > 2) {
+    if constexpr (!ROLL && WS::NP > 2 && TMG_RESET_RECOMP) {
         // 512-cell reset kernel: unrolled (the passes' loads overlap), the cell
         // geometry of each scanned pass rebuilt from an opaque lane index
         // instead of eight per-pass VGPRs kept across the redraw loop
@@ -1750,12 +1775,16 @@ struct Serial {
 // ensure-playable loop), which bounds the first line search.
 template <int MAXN, bool GEN, int SBNB, bool CODD, int TIER, class WS, class L>
 __device__ __forceinline__ int board_move(const Params &P, WS &w, int lane, const LaneJump &J, Rng &g,
-                          const Cells<MAXN / 64> &cl_unused, int p1, int p2, int &flags, int &nn, int &na, int64_t e,
+                          const Cells<MAXN / 64> &cl, int p1, int p2, int &flags, int &nn, int &na, int64_t e,
                           L *lists, bool clean) {
-    (void)cl_unused;
-    // the per-lane cell coordinates are rebuilt where they are used (a few
-    // VALU ops) rather than kept live across the cascade loop
-    const auto cells = [&]() { return make_cells<MAXN / 64>(P, loop_lane(lane)); };
+    // <= 128 cells: the per-lane cell coordinates are rebuilt where they are
+    // used (a few VALU ops) rather than kept live across the cascade loop,
+    // which spilled the 128-cell general kernels to scratch; 512 cells: eight
+    // passes' worth, kept (TMG_CELLS_ONCE)
+    const auto cells = [&]() {
+        if constexpr (MAXN > 128 && TMG_CELLS_ONCE) return cl;
+        else return make_cells<MAXN / 64>(P, loop_lane(lane));
+    };
     const int N = P.N;
     // Bound of the bottom-most line (detect's lim): after the swap of a
     // line-free board a line holds a swapped cell, so it is anchored at most two
@@ -1878,12 +1907,19 @@ __device__ __forceinline__ int board_move(const Params &P, WS &w, int lane, cons
 }
 
 // ------------------------------------------------------------------ kernels
+template <int MAXN = 128, bool LB = (MAXN > 128)>
 __device__ __forceinline__ LaneJump load_jump(const Params &P, int lane, const Rng &g) {
     const uint64_t *t = P.jump + lane * 4;
     LaneJump J;
     J.Aj = U128{t[0], t[1]};
     J.Gj = U128{t[2], t[3]};
     J.incG = mul128(U128{g.ilo, g.ihi}, J.Gj);
+    J.A64 = J.incG64 = U128{0, 0};
+    if constexpr (MAXN > 128 && LB) {                   // draws of > 128 colours span several batches
+        const uint64_t *u = P.jump + 63 * 4;             // A^64, G_64 (wave-uniform)
+        J.A64 = U128{u[0], u[1]};
+        J.incG64 = mul128(U128{g.ilo, g.ihi}, U128{u[2], u[3]});
+    }
     return J;
 }
 
@@ -1968,7 +2004,7 @@ __device__ __forceinline__ uint32_t step_env(
         effective = __ballot(ex) != 0ULL;
     }
     Rng g = load_rng(rng + e * 5);
-    const LaneJump J = load_jump(P, lane, g);
+    const LaneJump J = load_jump<MAXN, TMG_LANE_BATCH_STEP != 0>(P, lane, g);
     const Cells<MAXN / 64> cl = make_cells<MAXN / 64>(P, lane);
     int elim = 0, nn = 0, na = 0;
     bool changed = false;
@@ -2107,7 +2143,7 @@ __device__ __forceinline__ void reset_env(const Params &P, WS &w, int lane, int6
                                           uint64_t *__restrict__ eff) {
     const int N = P.N, W = P.W;
     Rng g = load_rng(rng + e * 5);
-    const LaneJump J = load_jump(P, lane, g);
+    const LaneJump J = load_jump<MAXN, TMG_LANE_BATCH != 0>(P, lane, g);
     const Cells<MAXN / 64> cl = make_cells<MAXN / 64>(P, lane);
     int fl;
     if constexpr (SBNB > 0) fl = sb_generate<SBNB, CODD, TMG_SB_VDET != 0>(P, w, lane, J, g, cl);   // board.py:95-109
