@@ -440,7 +440,7 @@ struct LaneJump {
     U128 A64, incG64;
 };
 #ifndef TMG_LANE_BATCH
-#define TMG_LANE_BATCH 1         // 512-cell reset kernel
+#define TMG_LANE_BATCH 0         // 512-cell reset kernel (1: measured slower, c5 1.12 vs 1.15 x 10^8)
 #endif
 #ifndef TMG_LANE_BATCH_STEP
 #define TMG_LANE_BATCH_STEP 0    // 512-cell step kernels (+5 VGPRs: 3 -> 2 waves/SIMD for the general one)
