@@ -275,7 +275,13 @@ def main():
         total = nb * world * args.steps
         value = total / el
         bpu = algorithmic_bytes_per_env_step(R, C)
-        achieved = bpu * nb / (step_ms * 1e-3) / 1e9          # one GPU's envs per step / its device time per step
+        # roofline.achieved: the dominant kernel's algorithmic bytes per launch
+        # (bpu x the envs one group launch steps) / its average launch duration
+        # (HIP events on group 0's stream, the stream the kernel runs on; for
+        # c3 / c5 that stream also carries the masked reset and spill launches
+        # of each step, so this is the step's whole per-group launch sequence)
+        achieved = bpu * launch_envs / (kern_ms * 1e-3) / 1e9
+        device_gbs = bpu * nb / (step_ms * 1e-3) / 1e9        # one GPU's envs per step / its device time per step
         smask = (1 if "cookie" in cl else 0) | (2 if "vertical_laser" in co else 0) | \
                 (4 if "horizontal_laser" in co else 0) | (8 if "bomb" in co else 0)
         cpu = None if (args.no_cpu_baseline or world > 1) else cpu_baseline(args.config, R, C, k, smask, moves,
@@ -325,7 +331,7 @@ def main():
                          "traffic_bytes_per_env_step": traffic.get("hbm_bytes_per_env_step") if traffic else None,
                          "algorithmic_bytes_per_env_step": bpu, "device_ms_per_step": round(step_ms, 4),
                          "kernel_ms_per_launch": round(kern_ms, 4), "envs_per_launch": launch_envs,
-                         "per_launch_gbs": round(bpu * launch_envs / (kern_ms * 1e-3) / 1e9, 2),
+                         "device_gbs": round(device_gbs, 2),
                          "issue": issue},
             "cpu_baseline": cpu,
             "build": {k: (v[:16] if k in ("src", "so_sha256") else v) for k, v in build.items() if k != "path"},

@@ -36,6 +36,26 @@ bench)
   timeout -k 10 300 python bench.py --steps 20 --warmup 5 --no-cpu-baseline > $OUT/c2_driver_window_bench.log 2>&1 || exit 1
   tail -1 $OUT/c2_driver_window_bench.log | cut -c1-200
   ;;
+probe)
+  # per-launch breakdown: quick-exit floor / normal step / autoreset storm, and a bare reset
+  for c in ${CONFIGS:-c2 c3 c5}; do
+    timeout -k 10 240 python tools/microbench.py --config $c > $OUT/${c}_microbench.log 2>&1 \
+      || { echo "microbench $c failed"; tail $OUT/${c}_microbench.log; exit 1; }
+    echo "$c $(tail -1 $OUT/${c}_microbench.log)"
+    timeout -k 10 240 python tools/reset_probe.py $c > $OUT/${c}_reset_probe.log 2>&1 \
+      || { echo "reset_probe $c failed"; tail $OUT/${c}_reset_probe.log; exit 1; }
+    tail -1 $OUT/${c}_reset_probe.log
+  done
+  ;;
+stamps)
+  # per-env phase durations from the TMG_STAMPS diagnostic build (make ... VARIANT=stamps STAMPS=1)
+  for c in ${CONFIGS:-c2}; do
+    TMG_LIB=$PWD/tile-match-gym_amd/tile_match_gym_amd/_lib/libtmg_stamps.so timeout -k 10 240 \
+      python tools/stamps.py --config $c --steps 60 > $OUT/${c}_stamps.log 2>&1 \
+      || { echo "stamps $c failed"; tail $OUT/${c}_stamps.log; exit 1; }
+    tail -8 $OUT/${c}_stamps.log
+  done
+  ;;
 all)
   STAGE=tests bash scripts/gpu_r03.sh && STAGE=deep bash scripts/gpu_r03.sh && STAGE=bench bash scripts/gpu_r03.sh
   ;;

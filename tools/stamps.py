@@ -28,7 +28,7 @@ def main():
     from tile_match_gym_amd import _native
     from tile_match_gym_amd.vec_env import TileMatchVecEnv
     L = _native.load()
-    L.tmg_debug_stamps.argtypes = [ctypes.c_void_p, ctypes.c_int64]
+    L.tmg_debug_stamps.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64]
     R, C, k, cl, co, nb, _ = bench.CONFIGS[args.config]
     nb = args.boards or min(nb, 1 << 18)
     env = TileMatchVecEnv(nb, R, C, k, 30, cl, co, seed=0, device="cuda:0")
@@ -40,7 +40,7 @@ def main():
     for t in range(args.steps):
         env.step_raw(acts[t])
         torch.cuda.synchronize()
-        assert L.tmg_debug_stamps(st.ctypes.data, nb) == 0
+        _native.check(L.tmg_debug_stamps(env.ctx.handle, st.ctypes.data, nb), L)
         rew = env.reward.cpu().numpy()
         fl = env.flags.cpu().numpy()
         s = st.astype(np.int64)
