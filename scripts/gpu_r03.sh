@@ -47,6 +47,43 @@ probe)
     tail -1 $OUT/${c}_reset_probe.log
   done
   ;;
+iter)
+  # one iteration: GPU parity suite (not the deep rollouts), then c2/c3/c5 bench lines (no CPU baseline) and the
+  # per-launch probes; AB="name ..." adds c2/c3 bench lines of _lib/libtmg_ab_<name>.so
+  TMG_EVIDENCE_DIR=$OUT/evidence timeout -k 10 900 $PYT tests -m gpu --ignore=tests/test_gpu_deep.py \
+    > $OUT/pytest_gpu.log 2>&1 || { echo "pytest failed"; tail -30 $OUT/pytest_gpu.log; exit 1; }
+  tail -1 $OUT/pytest_gpu.log
+  for c in ${CONFIGS:-c2 c3 c5}; do
+    timeout -k 10 300 python bench.py --config $c --no-cpu-baseline > $OUT/${c}_bench.log 2>&1 || { echo "bench $c failed"; tail $OUT/${c}_bench.log; exit 1; }
+    echo "$c $(tail -1 $OUT/${c}_bench.log | cut -c80-140)"
+    timeout -k 10 240 python tools/microbench.py --config $c > $OUT/${c}_microbench.log 2>&1 || { echo "microbench $c failed"; exit 1; }
+    echo "$c $(tail -1 $OUT/${c}_microbench.log)"
+  done
+  for ab in ${AB:-}; do
+    for c in c2 c3; do
+      TMG_LIB=$PWD/tile-match-gym_amd/tile_match_gym_amd/_lib/libtmg_ab_$ab.so timeout -k 10 300 python bench.py --config $c \
+        --no-cpu-baseline > $OUT/${c}_ab_${ab}_bench.log 2>&1 || { echo "bench ab $ab $c failed"; tail $OUT/${c}_ab_${ab}_bench.log; exit 1; }
+      echo "ab $ab $c $(tail -1 $OUT/${c}_ab_${ab}_bench.log | cut -c80-140)"
+    done
+  done
+  ;;
+abx)
+  # A/B: bench line + per-launch probes for the product library and each _lib/libtmg_ab_<name>.so in AB, twice
+  # each in alternating order (box noise)
+  for rep in 1 2; do
+    for ab in product ${AB:-}; do
+      lib=$PWD/tile-match-gym_amd/tile_match_gym_amd/_lib/libtmg.so
+      [ $ab != product ] && lib=$PWD/tile-match-gym_amd/tile_match_gym_amd/_lib/libtmg_ab_$ab.so
+      for c in ${CONFIGS:-c2 c3}; do
+        TMG_LIB=$lib timeout -k 10 300 python bench.py --config $c --no-cpu-baseline > $OUT/${c}_${ab}_${rep}_bench.log 2>&1 \
+          || { echo "bench $ab $c failed"; tail $OUT/${c}_${ab}_${rep}_bench.log; exit 1; }
+        TMG_LIB=$lib timeout -k 10 240 python tools/microbench.py --config $c > $OUT/${c}_${ab}_${rep}_micro.log 2>&1 \
+          || { echo "micro $ab $c failed"; exit 1; }
+        echo "$rep $ab $c $(tail -1 $OUT/${c}_${ab}_${rep}_bench.log | cut -c88-110) $(tail -1 $OUT/${c}_${ab}_${rep}_micro.log)"
+      done
+    done
+  done
+  ;;
 stamps)
   # per-env phase durations from the TMG_STAMPS diagnostic build (make ... VARIANT=stamps STAMPS=1)
   for c in ${CONFIGS:-c2}; do

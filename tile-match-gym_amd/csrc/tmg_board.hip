@@ -81,6 +81,9 @@ namespace tmg {
 #ifndef TMG_CELLS_ONCE
 #define TMG_CELLS_ONCE 1       // 512-cell board_move: cell geometry computed once per step (1) or rebuilt where used (0; c5 neutral)
 #endif
+#ifndef TMG_PREFETCH
+#define TMG_PREFETCH 1         // step prologue loads issued before the action is known (step_env)
+#endif
 #ifndef TMG_RESET512_WAVES
 #define TMG_RESET512_WAVES 5   // min waves per SIMD for the 512-cell reset kernel (caps its VGPRs; A/B 4 / 6 slower)
 #endif
@@ -299,7 +302,7 @@ struct WsCore {
     // neighbour reads at p - 2C (C <= 64) stay inside it without clamping
     static constexpr int PRE = MAXW * 8 + SC_COUNT * 4;
     int8_t lpad[PRE >= 128 ? 1 : 128 - PRE];
-    int8_t brd[2 * MAXN];          // [colour plane N][type plane N], runtime N (same layout as HBM)
+    alignas(4) int8_t brd[2 * MAXN];   // [colour plane N][type plane N], runtime N (same layout as HBM)
     uint8_t mark[MAXN];
     alignas(8) int8_t trash[4 * 64];   // target of predicated-off stores (keeps hot loops branch-free)
     union {
@@ -404,6 +407,10 @@ __device__ __forceinline__ int popc_below(uint64_t m) {
 // instead of being kept live, or spilled, across the whole loop.
 #ifndef TMG_OPAQUE_V
 #define TMG_OPAQUE_V(x) asm volatile("" : "+v"(x))
+#endif
+// a use of a VGPR value here (its load has to land before this point)
+#ifndef TMG_KEEP_V
+#define TMG_KEEP_V(x) asm volatile("" ::"v"(x))
 #endif
 __device__ __forceinline__ int loop_lane(int lane) {
     int l = lane;
@@ -599,6 +606,38 @@ __device__ __forceinline__ void load_board(const Params &P, WS &w, int lane, con
         for (int i = lane; i < nb; i += 64) w.brd[i] = src[i];
     }
 }
+// An env's board read into registers at the top of a step, before the
+// effectiveness test decides whether it is needed (one dword per lane and
+// 64-dword pass; boards with an odd cell count are not dword-aligned in HBM
+// and take load_board instead).
+template <int MAXN>
+struct BoardPre {
+    static constexpr int K = (2 * MAXN / 4 + 63) / 64;
+    uint32_t v[K];
+};
+template <int MAXN>
+__device__ __forceinline__ void board_prefetch(const Params &P, BoardPre<MAXN> &b, int lane, const int8_t *src) {
+    const int nw = (2 * P.N) >> 2;
+    const uint32_t *s = reinterpret_cast<const uint32_t *>(src);
+#pragma unroll
+    for (int k = 0; k < BoardPre<MAXN>::K; k++) {
+        const int i = k * 64 + lane;
+        b.v[k] = (!(P.N & 1) && i < nw) ? s[i] : 0u;
+    }
+}
+template <int MAXN, class WS>
+__device__ __forceinline__ void board_from_prefetch(const Params &P, WS &w, const BoardPre<MAXN> &b, int lane,
+                                                    const int8_t *src) {
+    if (P.N & 1) { load_board(P, w, lane, src); return; }
+    const int nw = (2 * P.N) >> 2;
+    uint32_t *d = reinterpret_cast<uint32_t *>(w.brd);
+#pragma unroll
+    for (int k = 0; k < BoardPre<MAXN>::K; k++) {
+        const int i = k * 64 + lane;
+        if (i < nw) d[i] = b.v[k];
+    }
+}
+
 template <class WS>
 __device__ __forceinline__ void store_board(const Params &P, const WS &w, int lane, int8_t *dst) {
     const int nb = 2 * P.N;
@@ -1928,6 +1967,13 @@ __device__ __forceinline__ Rng load_rng(const uint64_t *p) {
     g.slo = bcast64(p[0]); g.shi = bcast64(p[1]); g.ilo = bcast64(p[2]); g.ihi = bcast64(p[3]); g.h = bcast64(p[4]);
     return g;
 }
+// the same from a row read one word per lane (lane i holds word i)
+__device__ __forceinline__ Rng rng_from_row(uint64_t row) {
+    Rng g;
+    g.slo = rdlane64(row, 0); g.shi = rdlane64(row, 1); g.ilo = rdlane64(row, 2); g.ihi = rdlane64(row, 3);
+    g.h = rdlane64(row, 4);
+    return g;
+}
 __device__ __forceinline__ void store_rng(uint64_t *p, const Rng &g, int lane) {
     if (lane == 0) { p[0] = g.slo; p[1] = g.shi; p[2] = g.ilo; p[3] = g.ihi; p[4] = g.h; }
 }
@@ -1955,6 +2001,19 @@ __device__ __forceinline__ uint32_t step_env(
     STAMP(e, 0);
     const int a = __builtin_amdgcn_readfirstlane(actions[e]);             // wave-uniform loads
     const int t0 = __builtin_amdgcn_readfirstlane(timer[e]);
+    // Issued beside the two loads above, none depending on the action: the
+    // env's cached mask row (lane i holds word i) and its board words.  The
+    // ineffective-move exit then waits for one memory latency instead of the
+    // chain action -> mask word, and the effective path finds its board in
+    // registers.  (The mask row is allocated memory whatever trust_eff says;
+    // it is only read as a mask when trust_eff != 0.)
+    // TMG_PREFETCH: 0 = none (the mask word loaded once the action is known),
+    // 1 = the mask row, 2 = the mask row, board and RNG state
+    const uint64_t effrow = (TMG_PREFETCH >= 1 && lane < W) ? eff[e * W + lane] : 0ULL;
+    const uint64_t rngrow = (TMG_PREFETCH >= 2 && lane < 5) ? rng[e * 5 + lane] : 0ULL;   // lane i: RNG word i
+    BoardPre<MAXN> bpre;
+    if constexpr (TMG_PREFETCH >= 2) board_prefetch(P, bpre, lane, board + e * 2 * N);
+    if constexpr (TMG_PREFETCH >= 1) TMG_KEEP_V(effrow);
     if (t0 >= P.num_moves || a < 0 || a >= P.A) {                           // tile_match_env.py:94-95
         if (lane == 0) { reward[e] = 0; n_new[e] = 0; n_act[e] = 0; flags_out[e] = FL_ERR; }
         if (P.oh && !trust_eff) {             // the fused planes follow every board of an untrusted call
@@ -1970,7 +2029,10 @@ __device__ __forceinline__ uint32_t step_env(
     const bool done = t1 == P.num_moves;                                    // tile_match_env.py:100-101
     int flags = done ? FL_DONE : 0;
     bool effective = false;
-    if (trust_eff) effective = (bcast64(ge[a >> 6]) >> (a & 63)) & 1ULL;    // board.py:352 via cached mask
+    if (trust_eff) {                                                        // board.py:352 via cached mask
+        if constexpr (TMG_PREFETCH >= 1) effective = (rdlane64(effrow, a >> 6) >> (a & 63)) & 1ULL;
+        else effective = (bcast64(ge[a >> 6]) >> (a & 63)) & 1ULL;
+    }
     if (trust_eff && !effective && !(done && autoreset == 1)) {             // no state change at all
         const bool defer = done && autoreset;                               // autoreset == 2: reset_kernel next
         if (done && !defer) for (int i = lane; i < W; i += 64) ge[i] = 0ULL; // tile_match_env.py:119-120
@@ -1985,7 +2047,8 @@ __device__ __forceinline__ uint32_t step_env(
     action_coords(P.R, P.C, a, r1, c1, r2, c2);
     const int p1 = r1 * P.C + c1, p2 = r2 * P.C + c2;
 
-    load_board(P, w, lane, gb);
+    if constexpr (TMG_PREFETCH >= 2) board_from_prefetch(P, w, bpre, lane, gb);
+    else load_board(P, w, lane, gb);
     if constexpr (GEN) {
         for (int p = lane; p < N; p += 64) w.mark[p] = 0;
     }
@@ -2003,7 +2066,7 @@ __device__ __forceinline__ uint32_t step_env(
         bool ex = lane == 0 ? eff_exact(P, w.brd, a) : false;
         effective = __ballot(ex) != 0ULL;
     }
-    Rng g = load_rng(rng + e * 5);
+    Rng g = TMG_PREFETCH >= 2 ? rng_from_row(rngrow) : load_rng(rng + e * 5);
     const LaneJump J = load_jump<MAXN, TMG_LANE_BATCH_STEP != 0>(P, lane, g);
     const Cells<MAXN / 64> cl = make_cells<MAXN / 64>(P, lane);
     int elim = 0, nn = 0, na = 0;

@@ -75,4 +75,5 @@ inline unsigned emu_mbcnt_hi(unsigned m, unsigned acc) {
 
 #define TMG_CONST_AS
 #define TMG_KEEP_V3(x, y, z) ((void)0)
+#define TMG_KEEP_V(x) ((void)0)
 #define TMG_SMEM_DECL(name) unsigned char *name = emu_smem()
