@@ -152,6 +152,11 @@ def test_generate_golden_gpu():
     (3, 4, 2, 0, 2048, 45),
     (2, 63, 6, 0, 1024, 35),
     (11, 11, 4, 0, 2048, 45),
+    # > 128 cells and many colours: generated boards often need a shuffle, so
+    # the 512-cell reset kernel's colour ring hands over the exact stream
+    # position mid-generation (board.py:102-118)
+    (9, 15, 15, 0, 2048, 24),
+    (10, 14, 14, 0, 2048, 24),
 ])
 def test_oracle_parity_random_actions(cfg):
     """Batched random-action rollouts with autoreset vs the CPU oracle, every step."""

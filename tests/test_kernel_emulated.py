@@ -88,6 +88,35 @@ def test_random_rollouts_emulated(emu_lib, cfg):
             assert np.array_equal(getattr(e, f), getattr(o, f)), f"{cfg} step {t}: {f}"
 
 
+@pytest.mark.parametrize("cfg", [(9, 15, 15, 0), (10, 14, 14, 0)])
+def test_generate_shuffles_emulated(emu_lib, cfg):
+    """> 128-cell boards with many colours, where a generated line-free board
+    often has no effective move: the 512-cell reset kernel's colour ring hands
+    the exact stream position to shuffle (board.py:102-118) and resumes after it.
+    Emulated kernels vs the oracle, every field, after every reset and step."""
+    from oracle import oracle as orc
+    from tile_match_gym_amd.seeding import batch_rng_words
+    emu, L = emu_lib
+    R, C, k, sm = cfg
+    n, T = 48, 24
+    w = batch_rng_words(range(5000, 5000 + n))
+    e = emu.EmuBatch(L, R, C, k, sm, 3, w)
+    o = orc.OracleBatch(R, C, k, sm, 3, w)
+    e.reset()
+    o.reset()
+    rs = np.random.default_rng(R * 100 + C)
+    A = 2 * R * C - R - C
+    shuffled = 0
+    for t in range(-1, T):
+        if t >= 0:
+            a = rs.integers(0, A, n).astype(np.int32)
+            e.step(a, True)
+            o.step(a, True)
+            shuffled += int(((o.flags & 4) != 0).sum())
+        for f in ("board", "rng", "eff", "reward", "flags", "timer", "n_new", "n_act"):
+            assert np.array_equal(getattr(e, f), getattr(o, f)), f"{cfg} step {t}: {f}"
+
+
 def test_move_golden_emulated(emu_lib):
     """Board.move (board.py:330-395) from the recorded arbitrary boards (specials, coloured cookies,
     empties), through the emulated general kernel — the CPU twin of test_move_golden_gpu."""

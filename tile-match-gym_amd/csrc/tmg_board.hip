@@ -81,6 +81,9 @@ namespace tmg {
 #ifndef TMG_CELLS_ONCE
 #define TMG_CELLS_ONCE 1       // 512-cell board_move: cell geometry computed once per step (1) or rebuilt where used (0; c5 neutral)
 #endif
+#ifndef TMG_RESET_RING
+#define TMG_RESET_RING 1       // 512-cell reset kernel: generate_board's colours through the LDS colour ring
+#endif
 #ifndef TMG_PREFETCH
 #define TMG_PREFETCH 1         // step prologue loads issued before the action is known (step_env)
 #endif
@@ -1127,6 +1130,143 @@ __device__ __forceinline__ int generate_board(const Params &P, WS &w, int lane, 
     return ensure_playable<ROLL, PRE, true>(P, w, lane, J, g, cl) & FL_ERR;         // types all 1
 }
 
+// ---------------------------------------------------------------- colour ring
+// generate_board's colours (board.py:97, 129) are one sequence: every
+// Generator.integers(1, k+1, M) call takes the next M accepted 32-bit words of
+// the env's PCG64 stream (half-word buffer included), whatever M is.  The
+// 512-cell reset kernel therefore fills an LDS ring with that sequence, 64
+// outputs (128 colours) per batch, and each redraw takes its (row+1)*C
+// colours from it: every PCG64 jump-ahead then yields 128 used colours, where
+// a redraw of its own rounds its ~140 outputs up to three batches of 64.  The
+// exact stream position is recovered at the end (or before a shuffle) from the
+// latest batch's per-lane states.  A Lemire rejection anywhere in a batch
+// (Generator.integers' bounded draw, P.thr != 0) makes the caller redo the
+// board on the exact draw-by-draw path (generate_board), from the saved state.
+constexpr int kRing = 1024;                     // bytes: >= 512 cells + < 128 unconsumed
+struct ColourRing {
+    U128 fs;                                    // wave-uniform: state after the last output filled
+    U128 bs, bp;                                // wave-uniform: state before the latest / previous batch
+    int fill, cons, lbase;                      // ring indices (colours): filled, consumed, latest batch
+    int cons0;                                  // cons at ring_init: nothing taken while cons == cons0
+    bool rej;                                   // a rejected word was drawn (wave-uniform)
+};
+template <class WS>
+__device__ __forceinline__ uint8_t *ring_bytes(WS &w) { return reinterpret_cast<uint8_t *>(w.u.draw); }
+
+// The ring starting at stream position g: a buffered half-word (g.h) is the
+// first colour, at ring index 1, so every batch starts at an even index.
+template <class WS>
+__device__ __forceinline__ void ring_init(const Params &P, WS &w, int lane, const Rng &g, ColourRing &r) {
+    r.fs = U128{g.slo, g.shi};
+    r.bs = r.bp = r.fs;
+    r.fill = r.cons = 0;
+    r.lbase = 0;
+    r.rej = false;
+    if ((g.h >> 32) & 1) {
+        const uint64_t m = (uint64_t)(uint32_t)g.h * (uint32_t)P.k;
+        r.rej = (uint32_t)m < P.thr;
+        if (lane == 0) ring_bytes(w)[1] = (uint8_t)(1 + (m >> 32));
+        r.cons = 1;
+        r.fill = 2;
+    }
+    r.cons0 = r.cons;
+}
+
+template <class WS>
+__device__ __forceinline__ void ring_fill(const Params &P, WS &w, int lane, const LaneJump &J, ColourRing &r) {
+    const uint32_t k = (uint32_t)P.k;
+    const U128 sj = add128(mul128(J.Aj, r.fs), J.incG);              // output lane of the batch
+    const uint64_t out = xsl_rr(sj);
+    const uint64_t m0 = (uint64_t)(uint32_t)out * k, m1 = (out >> 32) * k;
+    const bool rj = ((uint32_t)m0 < P.thr) | ((uint32_t)m1 < P.thr);
+    if (P.thr != 0u && __ballot(rj) != 0ULL) r.rej = true;
+    uint16_t *ring = reinterpret_cast<uint16_t *>(ring_bytes(w));
+    ring[((r.fill >> 1) + lane) & (kRing / 2 - 1)] = (uint16_t)((1 + (m0 >> 32)) | ((1 + (m1 >> 32)) << 8));
+    r.bp = r.bs;
+    r.bs = r.fs;
+    r.lbase = r.fill;
+    r.fill += 128;
+    r.fs = U128{rdlane64(sj.lo, 63), rdlane64(sj.hi, 63)};
+}
+
+// dst[0..M) <- the next M colours (M <= 512)
+template <class WS>
+__device__ __forceinline__ void ring_take(const Params &P, WS &w, int lane, const LaneJump &J, ColourRing &r, int M,
+                                          int8_t *dst) {
+    while (r.fill - r.cons < M) ring_fill(P, w, lane, J, r);
+    WSYNC();
+    const uint8_t *ring = ring_bytes(w);
+    for (int i = lane; i < M; i += 64) dst[i] = (int8_t)ring[(r.cons + i) & (kRing - 1)];
+    r.cons += M;
+}
+
+// The exact PCG64 state after the last consumed colour.  It lies in one of
+// the two latest batches: a take leaves fewer than 128 colours unconsumed, and
+// at most one batch is filled ahead of the next take.
+// The batch's per-lane states are not kept: lane L's is recomputed from the
+// batch's starting state (one jump-ahead).
+__device__ __forceinline__ void ring_state(const LaneJump &J, const ColourRing &r, Rng &g) {
+    if (r.cons == r.cons0) return;                                   // nothing taken since ring_init(g)
+    int local = r.cons - 1 - r.lbase;
+    const bool prev = local < 0;
+    local += prev ? 128 : 0;
+    const int L = local >> 1;
+    const U128 sj = add128(mul128(J.Aj, prev ? r.bp : r.bs), J.incG);
+    const U128 s{rdlane64(sj.lo, L), rdlane64(sj.hi, L)};
+    g.slo = s.lo;
+    g.shi = s.hi;
+    g.h = ((uint64_t)((local & 1) ^ 1) << 32) | (uint32_t)(xsl_rr(s) >> 32);   // lo half taken: hi half buffered
+}
+
+// generate_board (board.py:95-109) on the colour ring, for the 512-cell reset
+// kernel; the loop is ensure_playable's with the redraws taken from the ring.
+// Returns FL_ERR when a safety cap was hit; on a Lemire rejection it returns
+// generate_board's result from the unchanged starting state.
+template <class WS>
+__device__ __forceinline__ int generate_board_ring(const Params &P, WS &w, int lane, const LaneJump &J, Rng &g,
+                                                   const Cells<WS::NP> &cl) {
+    const int N = P.N;
+    const Rng g0 = g;
+    ColourRing r;
+    ring_init(P, w, lane, g, r);
+    ring_take(P, w, lane, J, r, N, w.brd);
+    for (int p = lane; p < N; p += 64) w.brd[N + p] = 1;
+    WSYNC();
+    int fl = 0;
+    for (int shuffles = 0;; shuffles++) {
+        int lim = P.R - 1;
+        for (;;) {
+            if (r.fill - r.cons < 128) ring_fill(P, w, lane, J, r);   // the next redraw's first batch, beside the search
+            int ra = 0;
+            const int r0 = first_line_row<false, true>(P, w, lane, cl, lim, ra);
+            if (r0 < 0) break;
+            const int row = P.R - 1 < r0 + 1 ? P.R - 1 : r0 + 1;      // remove_colour_lines: rows 0..row
+            ring_take(P, w, lane, J, r, (row + 1) * P.C, w.brd);
+            WSYNC();
+            lim = min(P.R - 1, max(row + 2, ra));
+            if (r.rej) break;
+        }
+        if (r.rej) break;
+        if (scan_effective(P, w, lane, cl, true)) break;             // types all 1, line-free
+        if (shuffles >= TMG_MAX_SHUFFLES) { fl = FL_ERR; break; }
+        COVER(CV_SHUFFLE);
+        ring_state(J, r, g);                                         // shuffle draws from the stream itself
+        WSYNC();
+        shuffle(P, w, lane, g);
+        fl = FL_SHUF;
+        ring_init(P, w, lane, g, r);
+    }
+    if (r.rej) {                                                     // redo draw by draw (rare: P(reject) = thr / 2^32)
+        COVER(CV_REJECT);
+        g = g0;
+        WSYNC();
+        return generate_board<TMG_RESET_ROLL != 0, TMG_RESET_PRE != 0>(P, w, lane, J, g, cl);
+    }
+    ring_state(J, r, g);
+    WSYNC();
+    return fl & FL_ERR;
+}
+
 // Queue env e for spill_kernel.  The host sizes the queue for every env of
 // the launch, so this cannot fail; false only if that sizing were broken.
 __device__ __forceinline__ bool queue_env(SpillQ *q, int lane, int64_t e) {
@@ -2097,7 +2237,7 @@ __device__ __forceinline__ uint32_t step_env(
     if (done && autoreset) {                                                // reset() without a seed
         if constexpr (!LEAN_DEFER) {
             if (autoreset == 1) {
-                if constexpr (SBNB > 0) flags |= sb_generate<SBNB, CODD>(P, w, lane, J, g, cl);
+                if constexpr (SBNB > 0) flags |= sb_generate<SBNB, CODD, TMG_SB_VDET_STEP != 0>(P, w, lane, J, g, cl);
                 else flags |= generate_board(P, w, lane, J, g, cl);
                 changed = true;
             }
@@ -2210,6 +2350,7 @@ __device__ __forceinline__ void reset_env(const Params &P, WS &w, int lane, int6
     const Cells<MAXN / 64> cl = make_cells<MAXN / 64>(P, lane);
     int fl;
     if constexpr (SBNB > 0) fl = sb_generate<SBNB, CODD, TMG_SB_VDET != 0>(P, w, lane, J, g, cl);   // board.py:95-109
+    else if constexpr (MAXN > 128 && TMG_RESET_RING) fl = generate_board_ring(P, w, lane, J, g, cl);
     else fl = generate_board<TMG_RESET_ROLL != 0, TMG_RESET_PRE != 0>(P, w, lane, J, g, cl);
     note_status(P, lane, fl ? ST_INTERNAL : 0u);
     store_board(P, w, lane, board + e * 2 * N);

@@ -15,6 +15,9 @@
 #ifndef TMG_SB_VDET
 #define TMG_SB_VDET 1        // reset kernel: remove_colour_lines' line search on the lane codes (VALU)
 #endif
+#ifndef TMG_SB_VDET_STEP
+#define TMG_SB_VDET_STEP 1   // the same in the step kernels' inline autoreset (c2: 6.77 -> 7.24 x 10^8)
+#endif
 
 struct Pair {
     uint64_t a, b;
