@@ -2135,9 +2135,11 @@ __device__ __forceinline__ uint32_t step_env(
     int32_t *__restrict__ n_act, uint8_t *__restrict__ flags_out, uint64_t *__restrict__ eff, int trust_eff,
     int autoreset, L *lists) {
     const int N = P.N, W = P.W;
-    // the 128-cell lean kernels leave autoresets to a reset_kernel launch
-    // (TMG_LEAN_DEFER): no generate_board code in the hot step kernel
-    constexpr bool LEAN_DEFER = TMG_LEAN_DEFER && !GEN && MAXN == 128;
+    // Only the 128-cell lean kernels regenerate a finished board inline
+    // (autoreset == 1); do_step (tmg_capi.hip) hands every other kernel
+    // autoreset == 2, a masked reset_kernel launch after the step, so they
+    // carry no generate_board code (with TMG_LEAN_DEFER the lean ones neither)
+    constexpr bool INLINE_GEN = !GEN && MAXN == 128 && !TMG_LEAN_DEFER;
     STAMP(e, 0);
     const int a = __builtin_amdgcn_readfirstlane(actions[e]);             // wave-uniform loads
     const int t0 = __builtin_amdgcn_readfirstlane(timer[e]);
@@ -2235,7 +2237,7 @@ __device__ __forceinline__ uint32_t step_env(
     STAMP(e, 4);
     int tnew = t1;
     if (done && autoreset) {                                                // reset() without a seed
-        if constexpr (!LEAN_DEFER) {
+        if constexpr (INLINE_GEN) {
             if (autoreset == 1) {
                 if constexpr (SBNB > 0) flags |= sb_generate<SBNB, CODD, TMG_SB_VDET_STEP != 0>(P, w, lane, J, g, cl);
                 else flags |= generate_board(P, w, lane, J, g, cl);

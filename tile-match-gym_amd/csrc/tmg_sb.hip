@@ -15,6 +15,9 @@
 #ifndef TMG_SB_VDET
 #define TMG_SB_VDET 1        // reset kernel: remove_colour_lines' line search on the lane codes (VALU)
 #endif
+#ifndef TMG_SB_RING
+#define TMG_SB_RING 1        // generate_board's colours through the LDS colour ring (sb_generate)
+#endif
 #ifndef TMG_SB_VDET_STEP
 #define TMG_SB_VDET_STEP 1   // the same in the step kernels' inline autoreset (c2: 6.77 -> 7.24 x 10^8)
 #endif
@@ -499,12 +502,94 @@ __device__ __forceinline__ int sb_ensure(const Params &P, WS &w, int lane, const
 // generate_board, board.py:95-109 (types all 1; colours from the env stream);
 // returns FL_ERR when a safety cap was hit
 template <int NB, bool CODD, bool VDET = false, class WS>
-__device__ __forceinline__ int sb_generate(const Params &P, WS &w, int lane, const LaneJump &J, Rng &g,
-                                           const Cells<WS::NP> &cl) {
+__device__ __forceinline__ int sb_generate_exact(const Params &P, WS &w, int lane, const LaneJump &J, Rng &g,
+                                                 const Cells<WS::NP> &cl) {
     SBC c{0, 0};
     sb_draw_rows<NB>(P, w, lane, J, g, P.R - 1, c, sb_draw_pre(J, g));
     for (int p = lane; p < P.N; p += 64) w.brd[P.N + p] = 1;
     return sb_ensure<NB, CODD, VDET>(P, w, lane, J, g, cl, c, true, false) & FL_ERR;
+}
+
+// rows 0..M/C-1 of the lane codes <- the ring's next M colours (ring_take for
+// the lane-side board: lane j holds cells 2j and 2j+1)
+template <class WS>
+__device__ __forceinline__ void sb_ring_take(const Params &P, WS &w, int lane, const LaneJump &J, ColourRing &r, int M,
+                                             SBC &c) {
+    while (r.fill - r.cons < M) ring_fill(P, w, lane, J, r);
+    WSYNC();
+    const uint8_t *ring = ring_bytes(w);
+    const int q0 = 2 * lane;
+    const int x0 = ring[(r.cons + q0) & (kRing - 1)], x1 = ring[(r.cons + q0 + 1) & (kRing - 1)];
+    c.a = q0 < M ? x0 - 1 : c.a;
+    c.b = q0 + 1 < M ? x1 - 1 : c.b;
+    r.cons += M;
+}
+
+// generate_board (board.py:95-109) for the scalar-bitboard kernels with the
+// redraws' colours taken from the LDS colour ring (tmg_board.hip): a 10x10
+// redraw uses ~33 PCG64 outputs, where drawing it on its own costs a whole
+// 64-output jump-ahead batch.  The line search is sb_ensure's (lane codes,
+// VDET; bitboards otherwise).  A Lemire rejection redoes the board with
+// sb_generate_exact from the starting state.
+template <int NB, bool CODD, bool VDET = false, class WS>
+__device__ __forceinline__ int sb_generate(const Params &P, WS &w, int lane, const LaneJump &J, Rng &g,
+                                           const Cells<WS::NP> &cl) {
+    if constexpr (!TMG_SB_RING) return sb_generate_exact<NB, CODD, VDET>(P, w, lane, J, g, cl);
+    const Rng g0 = g;
+    int keyA, keyB;
+    sb_line_keys(P, lane, keyA, keyB);
+    int vokA = 0, vokB = 0, hokA = 0, hokB = 0;
+    if constexpr (VDET) {
+        vokA = (int)(P.sb_v[0] >> lane) & 1; vokB = (int)(P.sb_v[1] >> lane) & 1;
+        hokA = (int)(P.sb_h[0] >> lane) & 1; hokB = (int)(P.sb_h[1] >> lane) & 1;
+    }
+    ColourRing r;
+    ring_init(P, w, lane, g, r);
+    SBC c{0, 0};
+    sb_ring_take(P, w, lane, J, r, P.N, c);
+    for (int p = lane; p < P.N; p += 64) w.brd[P.N + p] = 1;
+    int fl = 0;
+    for (int shuffles = 0;; shuffles++) {
+        for (;;) {
+            if (r.fill - r.cons < 128) ring_fill(P, w, lane, J, r);   // the next redraw's batch, beside the search
+            int key, r0 = 0;
+            if constexpr (VDET) {
+                const SBVKey kv = sb_first_line_key_v<CODD>(P, c, lane, keyA, keyB, vokA, vokB, hokA, hokB);
+                key = kv.key;
+                if (key < 0) break;
+                r0 = sb_line_row_of_key_v(P, kv);
+            } else {
+                const SBDet d = sb_detect<NB, CODD>(P, sb_planes_of<NB>(c));
+                key = sb_first_line_key<NB, CODD>(P, d, lane, keyA, keyB);
+                if (key < 0) break;
+                r0 = sb_line_row_of_key<CODD>(P, d, key);
+            }
+            const int row = P.R - 1 < r0 + 1 ? P.R - 1 : r0 + 1;      // remove_colour_lines: rows 0..row
+            sb_ring_take(P, w, lane, J, r, (row + 1) * P.C, c);
+        }
+        if (r.rej) break;
+        WFENCE();
+        sb_codes_to_lds(P, w.brd, w.trash, lane, c);
+        WSYNC();
+        if (scan_effective_clean<false>(P, w, lane)) break;          // types all 1, no line
+        if (shuffles >= TMG_MAX_SHUFFLES) { fl = FL_ERR; break; }
+        COVER(CV_SHUFFLE);
+        ring_state(J, r, g);                                         // shuffle draws from the stream itself
+        WSYNC();
+        shuffle(P, w, lane, g);
+        c = sb_codes_from_lds(P, w.brd, lane);
+        fl = FL_SHUF;
+        ring_init(P, w, lane, g, r);
+    }
+    if (r.rej) {                                                     // redo draw by draw (P(reject) = thr / 2^32)
+        COVER(CV_REJECT);
+        g = g0;
+        WSYNC();
+        return sb_generate_exact<NB, CODD, VDET>(P, w, lane, J, g, cl);
+    }
+    ring_state(J, r, g);
+    WSYNC();
+    return fl & FL_ERR;
 }
 
 // Board.move, board.py:330-395, for a board that can hold no special (every
