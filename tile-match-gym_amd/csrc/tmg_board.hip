@@ -1189,14 +1189,23 @@ __device__ __forceinline__ void ring_fill(const Params &P, WS &w, int lane, cons
     r.fs = U128{rdlane64(sj.lo, 63), rdlane64(sj.hi, 63)};
 }
 
-// dst[0..M) <- the next M colours (M <= 512)
+// dst[0..M) <- the next M colours (M <= 512; dst 4-byte aligned): whole
+// dwords, each funnel-shifted out of the two ring dwords it straddles, then the
+// M % 4 tail bytes (the cells after dst[M) are kept)
 template <class WS>
 __device__ __forceinline__ void ring_take(const Params &P, WS &w, int lane, const LaneJump &J, ColourRing &r, int M,
                                           int8_t *dst) {
     while (r.fill - r.cons < M) ring_fill(P, w, lane, J, r);
     WSYNC();
     const uint8_t *ring = ring_bytes(w);
-    for (int i = lane; i < M; i += 64) dst[i] = (int8_t)ring[(r.cons + i) & (kRing - 1)];
+    const uint32_t *ring32 = reinterpret_cast<const uint32_t *>(ring);
+    uint32_t *dst32 = reinterpret_cast<uint32_t *>(dst);
+    const int nd = M >> 2, sh = r.cons & 3, q0 = r.cons >> 2;
+    for (int i = lane; i < nd; i += 64) {
+        const uint32_t lo = ring32[(q0 + i) & (kRing / 4 - 1)], hi = ring32[(q0 + i + 1) & (kRing / 4 - 1)];
+        dst32[i] = __builtin_amdgcn_alignbyte(hi, lo, (uint32_t)sh);
+    }
+    if (lane < (M & 3)) dst[(nd << 2) + lane] = (int8_t)ring[(r.cons + (nd << 2) + lane) & (kRing - 1)];
     r.cons += M;
 }
 

@@ -43,6 +43,8 @@ inline int emu_update_dpp(int old, int src, int ctrl, int row_mask, int bank_mas
 #define __builtin_amdgcn_readlane(v, l) ((int)emu_readlane((uint32_t)(v), (l)))
 #define __builtin_amdgcn_readfirstlane(v) ((int)emu_readlane((uint32_t)(v), 0))
 #define __builtin_amdgcn_ds_bpermute(a, v) ((int)emu_readlane((uint32_t)(v), ((a) >> 2) & 63))
+#define __builtin_amdgcn_alignbyte(a, b, s) \
+    ((uint32_t)(((((uint64_t)(uint32_t)(a)) << 32) | (uint32_t)(b)) >> (8 * ((s) & 3))))
 #define __builtin_amdgcn_fence(order, scope) emu_sync()
 #define __builtin_amdgcn_wave_barrier() ((void)0)
 inline void __syncthreads() { emu_sync(); }
