@@ -72,14 +72,18 @@ namespace tmg {
 #define TMG_RQ128_WAVES 5      // min waves per SIMD for the 128-cell reset-queue kernel (87 VGPRs, no spill)
 #endif
 #ifndef TMG_RESET_RECOMP
-// 512-cell reset kernel: 1 rebuilds the line search's cell geometry per pass
-// (79 VGPRs, no scratch, 6 waves/SIMD) instead of keeping it in VGPRs (96,
-// 88 B of scratch spills, 5 waves/SIMD); the rebuild's ~30 VALU per redraw
-// cost c5 10 % (1.04 vs 1.15 x 10^8): the kernel is VALU-bound
-#define TMG_RESET_RECOMP 0
+// 512-cell reset kernel: 1 rebuilds the byte line search's cell geometry per
+// pass (for C % 4 != 0; C % 4 == 0 takes first_line_row_dw) instead of keeping
+// it in VGPRs: 80 VGPRs, 6 waves/SIMD.  With the colour ring and the dword
+// search: c5 1.29 x 10^8 (0 at 5 waves/SIMD: 1.24; dword search off at
+// 5 waves/SIMD: 1.28)
+#define TMG_RESET_RECOMP 1
 #endif
 #ifndef TMG_CELLS_ONCE
 #define TMG_CELLS_ONCE 1       // 512-cell board_move: cell geometry computed once per step (1) or rebuilt where used (0; c5 neutral)
+#endif
+#ifndef TMG_RING_DWSEARCH
+#define TMG_RING_DWSEARCH 1    // 512-cell generate: remove_colour_lines' line search over dwords when C % 4 == 0
 #endif
 #ifndef TMG_RESET_RING
 #define TMG_RESET_RING 1       // 512-cell reset kernel: generate_board's colours through the LDS colour ring
@@ -88,7 +92,7 @@ namespace tmg {
 #define TMG_PREFETCH 1         // step prologue loads issued before the action is known (step_env)
 #endif
 #ifndef TMG_RESET512_WAVES
-#define TMG_RESET512_WAVES 5   // min waves per SIMD for the 512-cell reset kernel (caps its VGPRs; A/B 4 / 6 slower)
+#define TMG_RESET512_WAVES 6   // min waves per SIMD for the 512-cell reset kernel (caps its VGPRs; see TMG_RESET_RECOMP)
 #endif
 
 // compiler-only ordering point between a wave's LDS loads and later stores
@@ -980,6 +984,53 @@ __device__ __forceinline__ int first_line_row(const Params &P, const WS &w, int 
     return run_top(P, w, lane, rs, c0);                   // vertical: starts at the top of its run
 }
 
+// first_line_row for generate_board's boards (every type 1) when C % 4 == 0:
+// a lane takes one dword of the LDS colour plane, four cells of one row, so a
+// pass covers 256 cells.  The anchor tests of get_colour_lines
+// (board.py:163-193) become byte-wise: the dword against its funnel shifts by
+// one and two cells (horizontal) and against the dwords one and two rows up
+// (vertical); a zero byte of (x ^ y) | (x ^ z) is a triple (colours < 0x80, so
+// 0x80 - byte never borrows).  The lane's key is its leftmost anchor's, as in
+// first_line_row; passes are scanned bottom-up and stop one pass above the
+// first one holding an anchor.
+template <class WS>
+__device__ __forceinline__ int first_line_row_dw(const Params &P, const WS &w, int lane, int lim, int &ra) {
+    const int C = P.C, N = P.N, C4 = P.C >> 2, ND = P.N >> 2;
+    const uint32_t *b32 = reinterpret_cast<const uint32_t *>(w.brd);
+    const int last = min((lim + 1) * C, N) - 1;
+    const int ln = loop_lane(lane);
+    int best = -1, stop = -2;
+#pragma unroll
+    for (int i = (WS::MAXN / 4 + 63) / 64 - 1; i >= 0; i--) {
+        if (i * 256 > last || i < stop) continue;                       // wave-uniform
+        const int d = i * 64 + ln;
+        const bool in = d < ND;
+        const int dc = in ? d : 0;
+        const int r = div_c(P, 4 * dc), c0 = 4 * dc - r * C;
+        const uint32_t x = b32[dc], nx = b32[min(dc + 1, ND - 1)];
+        const uint32_t u1 = b32[max(dc - C4, 0)], u2 = b32[max(dc - 2 * C4, 0)];
+        const uint32_t n1 = __builtin_amdgcn_alignbyte(nx, x, 1u), n2 = __builtin_amdgcn_alignbyte(nx, x, 2u);
+        const uint32_t h = (x ^ n1) | (x ^ n2), v = (x ^ u1) | (x ^ u2);
+        const int hc = C - 2 - c0;                                      // cells of the dword that may start a run
+        const uint32_t hm = !in || hc <= 0 ? 0u : hc >= 4 ? 0x80808080u : 0x80808080u & ((1u << (8 * hc)) - 1u);
+        const uint32_t vm = in && r >= 2 ? 0x80808080u : 0u;
+        const uint32_t zh = (0x80808080u - h) & hm, zv = (0x80808080u - v) & vm;
+        const uint32_t any = zh | zv;
+        const int bi = (int)__builtin_ctz(any | 0x80000000u) >> 3;      // leftmost anchor byte
+        const int isv = (int)((zv >> (8 * bi + 7)) & 1u);
+        const int key = (((r & 63) << 8) | (255 - ((c0 + bi) & 255))) << 1 | isv;
+        best = max(best, any ? key : -1);
+        if (stop == -2 && __ballot(best >= 0) != 0ULL) stop = i - 1;
+    }
+    if (stop == -2) return -1;
+    const int key = wave_max(best);
+    const int rs = key >> 9;
+    ra = rs;
+    if (!(key & 1)) return rs;                                          // horizontal line at (rs, c0..)
+    const int c0 = 255 - ((key >> 1) & 255);
+    return run_top(P, w, lane, rs, c0);                                 // vertical: starts at the top of its run
+}
+
 // gravity, board.py:217-229 — stable partition of each column (empties to
 // the top).  Lanes are laid out column-major (64/R columns per pass) so one
 // ballot holds whole columns: a non-empty cell moves down by the popcount of
@@ -1247,7 +1298,8 @@ __device__ __forceinline__ int generate_board_ring(const Params &P, WS &w, int l
         for (;;) {
             if (r.fill - r.cons < 128) ring_fill(P, w, lane, J, r);   // the next redraw's first batch, beside the search
             int ra = 0;
-            const int r0 = first_line_row<false, true>(P, w, lane, cl, lim, ra);
+            const int r0 = (TMG_RING_DWSEARCH && !(P.C & 3)) ? first_line_row_dw(P, w, lane, lim, ra)
+                                                            : first_line_row<false, true>(P, w, lane, cl, lim, ra);
             if (r0 < 0) break;
             const int row = P.R - 1 < r0 + 1 ? P.R - 1 : r0 + 1;      // remove_colour_lines: rows 0..row
             ring_take(P, w, lane, J, r, (row + 1) * P.C, w.brd);
