@@ -117,6 +117,27 @@ def test_generate_shuffles_emulated(emu_lib, cfg):
             assert np.array_equal(getattr(e, f), getattr(o, f)), f"{cfg} step {t}: {f}"
 
 
+@pytest.mark.parametrize("cfg", [(10, 10, 6, 0), (9, 9, 5, 15), (20, 20, 6, 15), (16, 16, 6, 6), (9, 15, 15, 0)])
+def test_generate_lemire_rejection_emulated(emu_lib, cfg):
+    """generate_board whose very first 32-bit draw is a Lemire rejection
+    (tests/rejection_states.py): the colour-ring generators must detect it and
+    redo the board draw by draw — same board and RNG state as the oracle."""
+    from oracle import oracle as orc
+    from tile_match_gym_amd.seeding import batch_rng_words
+    from rejection_states import rejecting_words
+    emu, L = emu_lib
+    R, C, k, sm = cfg
+    n = 8
+    w = rejecting_words(batch_rng_words(range(300, 300 + n)))
+    e = emu.EmuBatch(L, R, C, k, sm, 30, w)
+    o = orc.OracleBatch(R, C, k, sm, 30, w)
+    e.reset()
+    o.reset()
+    for f in ("board", "rng", "eff", "timer"):
+        assert np.array_equal(getattr(e, f), getattr(o, f)), f"{cfg}: {f}"
+    assert not np.array_equal(o.rng, w), "the reset consumed the stream"
+
+
 def test_move_golden_emulated(emu_lib):
     """Board.move (board.py:330-395) from the recorded arbitrary boards (specials, coloured cookies,
     empties), through the emulated general kernel — the CPU twin of test_move_golden_gpu."""
