@@ -55,13 +55,16 @@ VALU_PEAK = 256 * 4 * CLOCK_HZ / 2
 SALU_PEAK = 256 * CLOCK_HZ
 
 CONFIGS = {
-    # name: (R, C, k, colourless, colour, boards per GPU, description)
-    "c2": (10, 10, 4, [], [], 65536, "65536 x 10x10 boards per GPU, 4 colours, no specials"),
-    "c3": (10, 10, 4, [], ["vertical_laser", "horizontal_laser", "bomb"], 262144,
-           "262144 x 10x10 boards per GPU, 4 colours, v/h-laser + bomb"),
-    "c5": (20, 20, 6, ["cookie"], ["vertical_laser", "horizontal_laser", "bomb"], 262144,
-           "262144 x 20x20 boards per GPU, 6 colours, all specials"),
+    # name: (R, C, k, colourless, colour, boards per GPU, what the specials are)
+    "c2": (10, 10, 4, [], [], 65536, "no specials"),
+    "c3": (10, 10, 4, [], ["vertical_laser", "horizontal_laser", "bomb"], 262144, "v/h-laser + bomb"),
+    "c5": (20, 20, 6, ["cookie"], ["vertical_laser", "horizontal_laser", "bomb"], 262144, "all specials"),
 }
+
+
+def workload_desc(R, C, k, nb, specials):
+    """The workload of a run as it was actually configured (--boards included)."""
+    return f"{nb} x {R}x{C} boards per GPU, {k} colours, {specials}"
 # The reference's own Python step() measured in the survey container (BASELINE.md §2,
 # 8 vCPU Xeon, numba absent): context for the CPU baseline, not a target.
 REF_PY = {"c2": (290, 1976), "c3": (281, 2421), "c5": (69, 492)}
@@ -132,15 +135,21 @@ def cpu_baseline(config, R, C, k, smask, moves, policy="uniform"):
                                                 "(BASELINE.md §2); context only"}}
 
 
-def load_profile(name, config):
+def load_profile(name, config, boards, groups):
+    """The committed rocprofv3 counts of `config` (profiles/<name>), only if
+    they were taken on a run of the same shape (boards per GPU, env groups);
+    counts of another run shape would not describe this line's launches."""
     p = os.path.join(ROOT, "profiles", name)
     if not os.path.exists(p):
         return None
     try:
         with open(p) as f:
-            return json.load(f).get(config)
+            prof = json.load(f).get(config)
     except Exception:
         return None
+    if not prof or prof.get("boards_per_gpu") != boards or prof.get("env_groups_per_gpu") != groups:
+        return None
+    return prof
 
 
 def spawn_ranks(n):
@@ -188,7 +197,7 @@ def main():
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
         sys.exit(spawn_ranks(args.gpus))
     world, rank, local_rank = dist_env()
-    R, C, k, cl, co, nb, desc = CONFIGS[args.config]
+    R, C, k, cl, co, nb, spdesc = CONFIGS[args.config]
     if args.boards:
         nb = args.boards
     rng_ = shard_range(rank, nb)
@@ -275,19 +284,20 @@ def main():
         total = nb * world * args.steps
         value = total / el
         bpu = algorithmic_bytes_per_env_step(R, C)
-        # roofline.achieved: the dominant kernel's algorithmic bytes per launch
-        # (bpu x the envs one group launch steps) / its average launch duration
-        # (HIP events on group 0's stream, the stream the kernel runs on; for
-        # c3 / c5 that stream also carries the masked reset and spill launches
-        # of each step, so this is the step's whole per-group launch sequence)
-        achieved = bpu * launch_envs / (kern_ms * 1e-3) / 1e9
-        device_gbs = bpu * nb / (step_ms * 1e-3) / 1e9        # one GPU's envs per step / its device time per step
+        # roofline.achieved: one GPU's algorithmic bytes per step (bpu x its
+        # envs) / the device time of that step (HIP events around the fork ...
+        # join of all env groups).  The groups' step launches run at the same
+        # time on their own streams, so one launch's bytes over its own
+        # duration (per_launch_gbs, comparable with rocprofv3's average for
+        # the step kernel) counts a third of the device's work per unit time.
+        achieved = bpu * nb / (step_ms * 1e-3) / 1e9
+        per_launch_gbs = bpu * launch_envs / (kern_ms * 1e-3) / 1e9
         smask = (1 if "cookie" in cl else 0) | (2 if "vertical_laser" in co else 0) | \
                 (4 if "horizontal_laser" in co else 0) | (8 if "bomb" in co else 0)
         cpu = None if (args.no_cpu_baseline or world > 1) else cpu_baseline(args.config, R, C, k, smask, moves,
                                                                              policy=args.policy)
         issue = None
-        prof = load_profile("issue.json", args.config) if args.policy == "uniform" else None
+        prof = load_profile("issue.json", args.config, nb, env.groups) if args.policy == "uniform" else None
         if prof:
             per_gpu = value / world
             v = prof["valu_per_env_step"] * per_gpu
@@ -297,7 +307,7 @@ def main():
                      "salu_peak": SALU_PEAK, "unit": "wave-instructions/s per GPU",
                      "valu_frac": round(v / VALU_PEAK, 4), "salu_frac": round(s / SALU_PEAK, 4),
                      "source": prof.get("source")}
-        traffic = load_profile("traffic.json", args.config) if args.policy == "uniform" else None
+        traffic = load_profile("traffic.json", args.config, nb, env.groups) if args.policy == "uniform" else None
         out = {
             "metric": METRIC,
             "value": round(value, 1),
@@ -314,7 +324,7 @@ def main():
                      if args.policy == "uniform" else
                      "synthetic (each step every env samples uniformly from its effective actions on device, "
                      "counter-based per (step, global env); seeds = global env index)"),
-            "config": {"workload": f"{args.config}: {desc}, num_moves=30, autoreset"
+            "config": {"workload": f"{args.config}: {workload_desc(R, C, k, nb, spdesc)}, num_moves=30, autoreset"
                                    + (", episodes aligned" if args.phase_blocks == 1 else
                                       ", every env's episode phase staggered (timer0 = env mod 30)" if args.phase_blocks <= 0
                                       else f", {args.phase_blocks} episode-phase blocks offset by "
@@ -331,7 +341,11 @@ def main():
                          "traffic_bytes_per_env_step": traffic.get("hbm_bytes_per_env_step") if traffic else None,
                          "algorithmic_bytes_per_env_step": bpu, "device_ms_per_step": round(step_ms, 4),
                          "kernel_ms_per_launch": round(kern_ms, 4), "envs_per_launch": launch_envs,
-                         "device_gbs": round(device_gbs, 2),
+                         "per_launch_gbs": round(per_launch_gbs, 2),
+                         # what limits the path: integer work whose
+                         # SALU / VALU issue and dependent chains (the redraw loop of
+                         # generate_board) bind long before HBM bandwidth
+                         "binding": "issue/latency (SALU + VALU issue, dependent per-board chains), not HBM",
                          "issue": issue},
             "cpu_baseline": cpu,
             "build": {k: (v[:16] if k in ("src", "so_sha256") else v) for k, v in build.items() if k != "path"},

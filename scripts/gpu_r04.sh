@@ -1,14 +1,16 @@
 #!/bin/bash
-# Round-3 GPU evidence.  Usage (through gpurun, from the repo root):
-#   STAGE=tests bash scripts/gpu_r03.sh   # pytest -m gpu (all but the deep rollouts), smoke, c2 bench
-#   STAGE=deep  bash scripts/gpu_r03.sh   # the deep rollouts vs the oracle + the TMG_COVER branch counts
-#   STAGE=bench bash scripts/gpu_r03.sh   # c2 / c3 / c5 bench lines with the CPU baseline + driver window
-#   STAGE=prof  bash scripts/gpu_r03.sh   # rocprofv3 --kernel-trace --stats of the c2 / c3 / c5 benches
-#   STAGE=all   bash scripts/gpu_r03.sh   # tests, deep, bench
+# Round-4 GPU evidence.  Usage (through gpurun, from the repo root):
+#   STAGE=tests bash scripts/gpu_r04.sh   # pytest -m gpu (all but the deep rollouts), smoke, c2 bench
+#   STAGE=deep  bash scripts/gpu_r04.sh   # the deep rollouts vs the oracle + the TMG_COVER branch counts
+#   STAGE=bench bash scripts/gpu_r04.sh   # c2 / c3 / c5 bench lines with the CPU baseline + driver window
+#   STAGE=prof  bash scripts/gpu_r04.sh   # rocprofv3 --kernel-trace --stats of the c2 / c3 / c5 benches
+#   STAGE=all   bash scripts/gpu_r04.sh   # tests, deep, bench
 # Each GPU step has its own time limit; the script stops at the first failure.
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
-TAG=${TAG:-r03}
+TAG=${TAG:-r04}
 OUT=gpurun_out/$TAG
+# LIB=libtmg_<x>.so: every step below runs that build of this tree (TMG_LIB)
+[ -n "${LIB:-}" ] && export TMG_LIB=$PWD/tile-match-gym_amd/tile_match_gym_amd/_lib/$LIB
 mkdir -p $OUT
 export TMPDIR=/tmp
 PYT="python -u -m pytest -x -v --timeout 240 --timeout-method thread"
@@ -70,7 +72,7 @@ iter)
 abx)
   # A/B: bench line + per-launch probes for the product library and each _lib/libtmg_ab_<name>.so in AB, twice
   # each in alternating order (box noise)
-  for rep in 1 2; do
+  for rep in $(seq 1 ${REPS:-2}); do
     for ab in product ${AB:-}; do
       lib=$PWD/tile-match-gym_amd/tile_match_gym_amd/_lib/libtmg.so
       [ $ab != product ] && lib=$PWD/tile-match-gym_amd/tile_match_gym_amd/_lib/libtmg_ab_$ab.so
@@ -85,17 +87,21 @@ abx)
   done
   ;;
 pmcmb)
-  # SQ instruction counts per launch kind (normal / storm / quick) of tools/microbench.py
+  # SQ instruction counts per launch kind (normal / storm / quick step launches, reset / spill launches) of
+  # tools/microbench.py; PMCLIBS="product ab_old": one set per library build
+  for lib in ${PMCLIBS:-product}; do
+  [ $lib != product ] && export TMG_LIB=$PWD/tile-match-gym_amd/tile_match_gym_amd/_lib/libtmg_$lib.so
   for c in ${CONFIGS:-c2}; do
     i=0
     for set in "SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_SMEM SQ_WAVES SQ_INSTS_BRANCH SQ_WAVE_CYCLES SQ_BUSY_CYCLES" \
                "SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_SCA SQ_WAIT_ANY SQ_ACTIVE_INST_ANY"; do
       i=$((i+1))
-      timeout -s KILL 120 rocprofv3 --pmc $set --kernel-trace -d $OUT/pmcmb_${c}_$i -o run --output-format csv -- \
-        python3 tools/microbench.py --config $c > $OUT/pmcmb_${c}_$i.log 2>&1 || { echo "pmc $c $i failed"; tail -5 $OUT/pmcmb_${c}_$i.log; exit 1; }
+      timeout -s KILL 150 rocprofv3 --pmc $set --kernel-trace -d $OUT/pmcmb_${lib}_${c}_$i -o run --output-format csv -- \
+        python3 tools/microbench.py --config $c ${BOARDS:+--boards $BOARDS} > $OUT/pmcmb_${lib}_${c}_$i.log 2>&1 || { echo "pmc $c $i failed"; tail -5 $OUT/pmcmb_${lib}_${c}_$i.log; exit 1; }
     done
-    nb=$(python3 -c "import bench; print(bench.CONFIGS['$c'][5])")
-    python3 tools/pmc_micro.py $OUT/pmcmb_${c}_1 $OUT/pmcmb_${c}_2 --boards $nb --eff-frac 0.24 > $OUT/pmcmb_${c}.json && cat $OUT/pmcmb_${c}.json
+    nb=${BOARDS:-$(python3 -c "import bench; print(bench.CONFIGS['$c'][5])")}
+    python3 tools/pmc_micro.py $OUT/pmcmb_${lib}_${c}_1 $OUT/pmcmb_${lib}_${c}_2 --boards $nb --eff-frac 0.24 > $OUT/pmcmb_${lib}_${c}.json && echo "$lib $c" && head -c 600 $OUT/pmcmb_${lib}_${c}.json
+  done
   done
   ;;
 stamps)
@@ -108,7 +114,7 @@ stamps)
   done
   ;;
 all)
-  STAGE=tests bash scripts/gpu_r03.sh && STAGE=deep bash scripts/gpu_r03.sh && STAGE=bench bash scripts/gpu_r03.sh
+  STAGE=tests bash scripts/gpu_r04.sh && STAGE=deep bash scripts/gpu_r04.sh && STAGE=bench bash scripts/gpu_r04.sh
   ;;
 prof)
   for c in ${CONFIGS:-c2 c3 c5}; do

@@ -161,3 +161,43 @@ def test_move_golden_emulated(emu_lib):
             assert (b.reward[i], b.n_new[i], b.n_act[i]) == (res[0], res[2], res[3]), f"counters {(R, C, k, sm)} rec {i}"
         total += n
     assert total > 500
+
+
+@pytest.mark.parametrize("name", ["c5_20x20k6", "gen_512_11x12k10", "gen_sb_6x6k7", "lean_512_9x15k15",
+                                  "lean_sb_5x6k7", "wide_512_3x45k7"])
+def test_rare_paths_emulated(emu_lib, name):
+    """tests/test_gpu_paths.py's rollouts (effective-action policy, short
+    episodes, crafted Lemire rejections before every 5th step) on the emulated
+    kernels vs the oracle, and each listed site (in-move / generate shuffles,
+    draw_colours replays, row-plane generate redos) hit."""
+    from oracle import oracle as orc
+    from oracle.policy_np import sample_effective_np
+    from rejection_states import words_rejecting_at
+    from test_gpu_paths import MOVES, VARIANTS, _inject
+    from tile_match_gym_amd._native import COVER_NAMES
+    from tile_match_gym_amd.seeding import batch_rng_words
+    emu, L = emu_lib
+    R, C, k, sm, _, _, sites = VARIANTS[name]
+    n, T = 96, 30
+    w = batch_rng_words(range(n))
+    e = emu.EmuBatch(L, R, C, k, sm, MOVES, w)
+    o = orc.OracleBatch(R, C, k, sm, MOVES, w)
+    emu.cover(L, True)
+    e.reset()
+    o.reset()
+    rs = np.random.default_rng(1)
+    A = 2 * R * C - R - C
+    for t in range(T):
+        inj = _inject(t, n, rs)
+        if inj is not None:
+            ww = words_rejecting_at(o.rng, inj[0], buffered=inj[1])
+            o.rng[:] = ww
+            e.rng[:] = ww
+        a = sample_effective_np(o.eff, A, 7, 0, t)
+        e.step(a, True)
+        o.step(a, True)
+        for f in ("board", "rng", "eff", "reward", "flags", "timer", "n_new", "n_act"):
+            assert np.array_equal(getattr(e, f), getattr(o, f)), (name, t, f)
+    hits = dict(zip(COVER_NAMES, emu.cover(L, True)))
+    missing = [s for s in sites if s != "shuffle_gen" and hits[s] == 0]
+    assert not missing, (name, {s: int(hits[s]) for s in sites})

@@ -163,9 +163,11 @@ enum : int {
     CV_COMBO,            // combination_match
     CV_SPILL,            // step queued for spill_kernel
     CV_SPILL_RUN,        // step re-run by spill_kernel
-    CV_SHUFFLE,          // shuffle in the ensure-playable loop
-    CV_REJECT,           // Lemire rejection: serial replay of a draw batch
+    CV_SHUFFLE,          // shuffle in a move's ensure-playable loop (board.py:381-391)
+    CV_REJECT,           // Lemire rejection: serial replay of a draw batch (draw_colours)
     CV_FAST,             // fast_clear step (general kernel, no specials enabled)
+    CV_SHUFFLE_GEN,      // shuffle in generate_board's loop (board.py:102-106)
+    CV_REJECT_GEN,       // Lemire rejection in the row-plane generate (bp_generate): exact redo
     CV_COUNT = 32
 };
 #if TMG_COVER
@@ -204,6 +206,22 @@ struct Params {
     unsigned long long *cover;    // TMG_COVER builds: CV_COUNT hit counters (null otherwise)
     uint64_t *stamps;             // TMG_STAMPS builds: per-env phase stamps (null otherwise)
 };
+
+// The kernels take Params by value as their FIRST argument and read it
+// through the kernarg segment pointer, field by field where each is used.
+// Used as a by-value argument, the whole block is loaded into SGPRs in the
+// entry block (AMDGPULowerKernelArguments) and spilled to VGPR lanes before
+// anything else runs, e.g. before the ineffective-move exit of a step.
+#ifndef TMG_KARG
+#define TMG_KARG 1             // A/B only (0: Params used as the by-value argument)
+#endif
+#ifndef TMG_KERNARG_PARAMS
+#if defined(__HIP_DEVICE_COMPILE__) && TMG_KARG
+#define TMG_KERNARG_PARAMS(p) (*(const Params *)__builtin_amdgcn_kernarg_segment_ptr())
+#else
+#define TMG_KERNARG_PARAMS(p) (p)          // the host pass of the kernel templates (never executed)
+#endif
+#endif
 
 // host: the per-row masks of Params::sb_rows (boards of <= 128 cells)
 inline void build_sb_rows(int R, int C, uint64_t *tab) {
@@ -312,8 +330,8 @@ struct WsCore {
     alignas(4) int8_t brd[2 * MAXN];   // [colour plane N][type plane N], runtime N (same layout as HBM)
     uint8_t mark[MAXN];
     alignas(8) int8_t trash[4 * 64];   // target of predicated-off stores (keeps hot loops branch-free)
-    union {
-        uint32_t draw[MAXN + 128];                  // refill colours
+    union alignas(16) {
+        uint32_t draw[MAXN + 128];                  // refill colours; generate_board's colour ring (bp_ring)
         struct { int8_t tmp[2 * MAXN]; int16_t perm[MAXN]; } sh;   // shuffle
     } u;
 };
@@ -1134,7 +1152,7 @@ __device__ __forceinline__ void shuffle(const Params &P, WS &w, int lane, Rng &g
 // PRE: the next redraw's first 64 PCG outputs are evaluated before the line
 // search (they depend only on the stream position), so the jump-ahead's VALU
 // chain issues beside the search's LDS reads.
-template <bool ROLL = true, bool PRE = false, bool ALL1 = false, class WS>
+template <bool ROLL = true, bool PRE = false, bool ALL1 = false, bool GEN = false, class WS>
 __device__ __forceinline__ int ensure_playable(const Params &P, WS &w, int lane, const LaneJump &J, Rng &g,
                                 const Cells<WS::NP> &cl, bool noline = false) {
     int fl = 0;
@@ -1161,7 +1179,7 @@ __device__ __forceinline__ int ensure_playable(const Params &P, WS &w, int lane,
         // here, so the scan needs no precheck
         if (scan_effective(P, w, lane, cl, ALL1 || (P.smask & SP_COOKIE) == 0)) break;
         if (shuffles >= TMG_MAX_SHUFFLES) return fl | FL_ERR;
-        COVER(CV_SHUFFLE);
+        COVER(GEN ? CV_SHUFFLE_GEN : CV_SHUFFLE);
         WSYNC();
         shuffle(P, w, lane, g);
         fl = FL_SHUF;
@@ -1178,7 +1196,7 @@ __device__ __forceinline__ int generate_board(const Params &P, WS &w, int lane, 
     draw_colours(P, lane, J, g, N, w.brd, w.trash);
     for (int p = lane; p < N; p += 64) w.brd[N + p] = 1;
     WSYNC();
-    return ensure_playable<ROLL, PRE, true>(P, w, lane, J, g, cl) & FL_ERR;         // types all 1
+    return ensure_playable<ROLL, PRE, true, true>(P, w, lane, J, g, cl) & FL_ERR;   // types all 1
 }
 
 // ---------------------------------------------------------------- colour ring
@@ -1324,6 +1342,264 @@ __device__ __forceinline__ int generate_board_ring(const Params &P, WS &w, int l
         return generate_board<TMG_RESET_ROLL != 0, TMG_RESET_PRE != 0>(P, w, lane, J, g, cl);
     }
     ring_state(J, r, g);
+    WSYNC();
+    return fl & FL_ERR;
+}
+
+// ------------------------------------------------------------ row bit-planes
+// generate_board (board.py:95-131) with one board row per lane, for boards of
+// C <= 32 columns (every reset and autoreset path): lane r < R holds NB
+// bit-planes of row r, bit c of plane b = bit b of (colour - 1) of cell (r, c)
+// (colours 1..k, k <= 15); lanes >= R hold 0.  remove_colour_lines' line
+// search (get_colour_lines' first pass, :158-193, every type 1) is then a few
+// VALU ops on the lane's own row plus one DPP wave_shr:1 for the row above:
+//   neR = OR_b P_b ^ (P_b >> 1)          (cell c differs from c + 1)
+//   h   = ~(neR | neR >> 1) & cols<=C-3  (a horizontal run of 3 starts at c)
+//   eqU = ~OR_b P_b ^ P_b[r-1]            (cell (r, c) equals (r-1, c))
+//   v   = eqU & eqU[r-1] & rows>=2        (a vertical run of 3 ends at (r, c))
+// The first line of get_colour_lines is in the bottom-most row holding an
+// anchor (one ballot), at its leftmost anchor column, vertical before
+// horizontal; a vertical line starts at the top of its run (one ballot of
+// eqU's column).  No LDS access in the search at all.
+//
+// The colours come from the env's stream as one sequence: every
+// Generator.integers(1, k+1, M) call takes the next M colours of it (:97,
+// :129), whatever M is, so each jump-ahead batch of 64 PCG64 outputs appends
+// 128 colours to a 1024-colour ring held as NB bit-strings in LDS (colour i
+// is bit i mod 1024 of each plane's string), and a redraw of rows 0..row
+// hands lane r its C colours [cons + rC, cons + rC + C) as one funnel shift
+// (v_alignbit) of two ring dwords per plane.  Batches start at multiples of
+// 128 (a buffered half-word, the sequence's first colour, sits at index 127),
+// so a batch's planes are four whole dwords each, and its starting PCG64
+// state goes to one of 8 LDS slots, from which the exact stream position is
+// recovered at the end.
+#ifndef TMG_BP
+#define TMG_BP 1               // A/B only (0: the round-3 byte colour ring), removed after the measurement
+#endif
+constexpr int kBpRingDw = 32;                    // dwords per plane string (1024 colours)
+constexpr int kBpPlaneDw = 36;                   // + a guard copy of dwords 0..3, so [d, d+1] never wraps
+template <int NB>
+struct RowPlanes {
+    uint32_t p[NB];
+};
+struct BpRing {
+    U128 fs;                                     // wave-uniform: state after the last output filled
+    int fill, cons, cons0;                       // colour indices: filled, consumed, consumed at init
+    bool rej;                                    // a rejected word was drawn (wave-uniform)
+};
+template <class WS>
+__device__ __forceinline__ uint32_t *bp_ring(WS &w) { return reinterpret_cast<uint32_t *>(w.u.draw); }   // [4][36]
+template <class WS>
+__device__ __forceinline__ uint32_t *bp_slots(WS &w) { return reinterpret_cast<uint32_t *>(w.u.draw) + 4 * kBpPlaneDw; }   // [8][4]
+
+template <int NB, class WS>
+__device__ __forceinline__ void bp_ring_init(const Params &P, WS &w, int lane, const Rng &g, BpRing &r) {
+    r.fs = U128{g.slo, g.shi};
+    r.fill = r.cons = 0;
+    r.rej = false;
+    if ((g.h >> 32) & 1) {                                   // the buffered half-word is colour 127
+        const uint64_t m = (uint64_t)(uint32_t)g.h * (uint32_t)P.k;
+        r.rej = (uint32_t)m < P.thr;
+        const uint32_t code = (uint32_t)(m >> 32);
+        uint32_t *ring = bp_ring(w);
+        if (lane == 0) {
+#pragma unroll
+            for (int b = 0; b < NB; b++) ring[b * kBpPlaneDw + 3] = ((code >> b) & 1u) << 31;
+        }
+        r.cons = 127;
+        r.fill = 128;
+    }
+    r.cons0 = r.cons;
+}
+
+// the next 128 colours (64 PCG64 outputs by jump-ahead, Lemire-32 on each
+// half) appended to the plane strings: lane l fetches the codes of colours l
+// and 64 + l (output l >> 1, half l & 1), and one ballot per plane and half
+// gives the batch's bits in sequence order; lane 0 stores them and the
+// batch's starting state
+template <int NB, class WS>
+__device__ __forceinline__ void bp_ring_fill(const Params &P, WS &w, int lane, const LaneJump &J, BpRing &r) {
+    const uint32_t k = (uint32_t)P.k;
+    const U128 sj = add128(mul128(J.Aj, r.fs), J.incG);
+    const uint64_t out = xsl_rr(sj);
+    const uint64_t m0 = (uint64_t)(uint32_t)out * k, m1 = (out >> 32) * k;
+    if (P.thr != 0u) {
+        const bool rj = ((uint32_t)m0 < P.thr) | ((uint32_t)m1 < P.thr);
+        if (__ballot(rj) != 0ULL) r.rej = true;
+    }
+    const int pk = (int)((m0 >> 32) | ((m1 >> 32) << 4));       // codes of colours 2*lane, 2*lane+1
+    const int sh = (lane & 1) << 2;
+    const int x0 = __builtin_amdgcn_ds_bpermute((lane >> 1) << 2, pk) >> sh;
+    const int x1 = __builtin_amdgcn_ds_bpermute((32 + (lane >> 1)) << 2, pk) >> sh;
+    uint64_t b0[NB], b1[NB];
+#pragma unroll
+    for (int b = 0; b < NB; b++) {
+        b0[b] = __ballot((x0 >> b) & 1);
+        b1[b] = __ballot((x1 >> b) & 1);
+    }
+    const int q = (r.fill >> 5) & (kBpRingDw - 1);
+    if (lane == 0) {
+        uint32_t *ring = bp_ring(w);
+#pragma unroll
+        for (int b = 0; b < NB; b++) {
+            uint64_t *d = reinterpret_cast<uint64_t *>(ring + b * kBpPlaneDw + q);
+            d[0] = b0[b];
+            d[1] = b1[b];
+            if (q == 0) { d[kBpRingDw / 2] = b0[b]; d[kBpRingDw / 2 + 1] = b1[b]; }   // guard copy
+        }
+        uint64_t *slot = reinterpret_cast<uint64_t *>(bp_slots(w) + 4 * ((r.fill >> 7) & 7));
+        slot[0] = r.fs.lo;
+        slot[1] = r.fs.hi;
+    }
+    r.fill += 128;
+    r.fs = U128{rdlane64(sj.lo, 63), rdlane64(sj.hi, 63)};
+}
+
+// The exact PCG64 state after the last consumed colour: lane L of the batch
+// holding it, recomputed from that batch's starting state (its LDS slot).
+template <class WS>
+__device__ __forceinline__ void bp_ring_state(const LaneJump &J, WS &w, const BpRing &r, Rng &g) {
+    if (r.cons == r.cons0) return;                                   // nothing taken since bp_ring_init(g)
+    const int i = r.cons - 1, local = i & 127;                       // i >= 128: a take draws >= 2 colours
+    WSYNC();
+    const uint32_t *st = bp_slots(w) + 4 * ((i >> 7) & 7);
+    const U128 b{((uint64_t)__builtin_amdgcn_readfirstlane(st[1]) << 32) | (uint32_t)__builtin_amdgcn_readfirstlane(st[0]),
+                 ((uint64_t)__builtin_amdgcn_readfirstlane(st[3]) << 32) | (uint32_t)__builtin_amdgcn_readfirstlane(st[2])};
+    const U128 sj = add128(mul128(J.Aj, b), J.incG);
+    const U128 s{rdlane64(sj.lo, local >> 1), rdlane64(sj.hi, local >> 1)};
+    g.slo = s.lo;
+    g.shi = s.hi;
+    g.h = ((uint64_t)((local & 1) ^ 1) << 32) | (uint32_t)(xsl_rr(s) >> 32);   // lo half taken: hi half buffered
+}
+
+// rows 0..row <- the ring's next (row + 1) * C colours (colour plane only)
+template <int NB, class WS>
+__device__ __forceinline__ void bp_take(const Params &P, WS &w, int lane, const LaneJump &J, BpRing &r, int row,
+                                        uint32_t cm, RowPlanes<NB> &pl) {
+    const int M = (row + 1) * P.C;
+    while (r.fill - r.cons < M) bp_ring_fill<NB>(P, w, lane, J, r);
+    WSYNC();
+    const uint32_t *ring = bp_ring(w);
+    const int o = r.cons + lane * P.C;                           // this lane's row starts here
+    const int d = (o >> 5) & (kBpRingDw - 1);
+    const uint32_t s = (uint32_t)o & 31u;
+    const uint32_t in = lane <= row ? cm : 0u;                   // the cells this take rewrites
+#pragma unroll
+    for (int b = 0; b < NB; b++) {
+        const uint32_t v = __builtin_amdgcn_alignbit(ring[b * kBpPlaneDw + d + 1], ring[b * kBpPlaneDw + d], s);
+        pl.p[b] = (v & in) | (pl.p[b] & ~in);
+    }
+    r.cons += M;
+}
+
+// The row of the first coord of the first line get_colour_lines would return
+// (remove_colour_lines, board.py:120-131), or -1 when it returns [].
+// hml / vml: this lane's valid horizontal-start / vertical-anchor columns.
+template <int NB>
+__device__ __forceinline__ int bp_first_line_row(const RowPlanes<NB> &pl, uint32_t hml, uint32_t vml) {
+    uint32_t neR = 0, neU = 0;
+#pragma unroll
+    for (int b = 0; b < NB; b++) {
+        const uint32_t x = pl.p[b];
+        neR |= x ^ (x >> 1);
+        neU |= x ^ (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x138, 0xf, 0xf, true);   // wave_shr:1: row r-1
+    }
+    const uint32_t eqU = ~neU;
+    const uint32_t h = ~(neR | (neR >> 1)) & hml;
+    const uint32_t v = eqU & (uint32_t)__builtin_amdgcn_update_dpp(0, (int)eqU, 0x138, 0xf, 0xf, true) & vml;
+    const uint32_t any = h | v;
+    const uint64_t rows = __ballot(any != 0u);
+    if (!rows) return -1;
+    const int rs = 63 - __clzll(rows);                           // bottom-most row holding a line
+    const uint32_t av = (uint32_t)__builtin_amdgcn_readlane((int)any, rs);
+    const uint32_t vv = (uint32_t)__builtin_amdgcn_readlane((int)v, rs);
+    const int c0 = __builtin_ctz(av);                            // leftmost line, vertical checked first
+    if (!((vv >> c0) & 1u)) return rs;                           // horizontal: starts at (rs, c0)
+    const uint64_t m = __ballot((eqU >> c0) & 1u);               // (r, c0) == (r-1, c0)
+    const uint64_t low = rs >= 63 ? ~0ULL : (2ULL << rs) - 1ULL;
+    return 63 - __clzll((~m & low) | 1ULL);                       // vertical: the top of its run
+}
+
+// the LDS colour plane from the row planes (cell p: row r's planes by bpermute)
+template <int NB, class WS>
+__device__ __forceinline__ void bp_to_lds(const Params &P, WS &w, int lane, const RowPlanes<NB> &pl) {
+    const int N = P.N, C = P.C;
+#pragma unroll
+    for (int i = 0; i < WS::NP; i++) {
+        if (i * 64 >= N) break;                                  // wave-uniform
+        const int p = min(i * 64 + lane, N - 1);
+        const int r = div_c(P, p), c = p - r * C;
+        int code = 0;
+#pragma unroll
+        for (int b = 0; b < NB; b++) code |= (int)((((uint32_t)__builtin_amdgcn_ds_bpermute(r << 2, (int)pl.p[b])) >> c) & 1u) << b;
+        if (i * 64 + lane < N) w.brd[p] = (int8_t)(code + 1);
+    }
+}
+
+// the row planes from the LDS colour plane (after a shuffle)
+template <int NB, class WS>
+__device__ __forceinline__ RowPlanes<NB> bp_from_lds(const Params &P, const WS &w, int lane) {
+    RowPlanes<NB> pl;
+#pragma unroll
+    for (int b = 0; b < NB; b++) pl.p[b] = 0;
+    const int r = lane < P.R ? lane : 0;
+    for (int c = 0; c < P.C; c++) {
+        const uint32_t x = lane < P.R ? (uint32_t)(w.brd[r * P.C + c] - 1) : 0u;
+#pragma unroll
+        for (int b = 0; b < NB; b++) pl.p[b] |= ((x >> b) & 1u) << c;
+    }
+    return pl;
+}
+
+// generate_board (board.py:95-109) on row bit-planes (C <= 32, colours of at
+// most NB planes).  Returns FL_ERR when the shuffle cap was hit, 0 otherwise;
+// -1 on a Lemire rejection anywhere in the colours drawn (Generator.integers'
+// bounded draw, p = thr / 2^32 per word): g is then back at its starting
+// state and the caller redoes the board on an exact draw-by-draw path.
+// Leaves the board in LDS (colour plane; types 1) and its mask in w.effw.
+template <int NB, class WS>
+__device__ __forceinline__ int bp_generate(const Params &P, WS &w, int lane, const LaneJump &J, Rng &g) {
+    const int R = P.R, C = P.C, N = P.N;
+    const Rng g0 = g;
+    const uint32_t cm = C >= 32 ? ~0u : (1u << C) - 1u;
+    const uint32_t hml = (lane < R && C >= 3) ? cm >> 2 : 0u;          // columns <= C-3
+    const uint32_t vml = (lane >= 2 && lane < R) ? cm : 0u;            // rows >= 2
+    for (int p = lane; p < N; p += 64) w.brd[N + p] = 1;
+    BpRing r;
+    bp_ring_init<NB>(P, w, lane, g, r);
+    RowPlanes<NB> pl;
+#pragma unroll
+    for (int b = 0; b < NB; b++) pl.p[b] = 0;
+    bp_take<NB>(P, w, lane, J, r, R - 1, cm, pl);                       // :97
+    int fl = 0;
+    for (int shuffles = 0;; shuffles++) {
+        for (;;) {                                                       // remove_colour_lines, :120-131
+            if (r.fill - r.cons < 128) bp_ring_fill<NB>(P, w, lane, J, r);   // the next redraw's colours, beside the search
+            const int r0 = bp_first_line_row<NB>(pl, hml, vml);
+            if (r0 < 0) break;
+            bp_take<NB>(P, w, lane, J, r, R - 1 < r0 + 1 ? R - 1 : r0 + 1, cm, pl);   // rows 0..min(R-1, r0+1)
+            if (r.rej) break;
+        }
+        if (r.rej) break;
+        bp_to_lds<NB>(P, w, lane, pl);
+        WSYNC();
+        if (scan_effective_clean<false>(P, w, lane)) break;             // possible_move, :102
+        if (shuffles >= TMG_MAX_SHUFFLES) { fl = FL_ERR; break; }
+        COVER(CV_SHUFFLE_GEN);
+        bp_ring_state(J, w, r, g);                                       // shuffle draws from the stream itself
+        WSYNC();
+        shuffle(P, w, lane, g);                                          // :105-106
+        pl = bp_from_lds<NB>(P, w, lane);
+        fl = FL_SHUF;
+        bp_ring_init<NB>(P, w, lane, g, r);
+    }
+    if (r.rej) {
+        COVER(CV_REJECT_GEN);
+        g = g0;
+        WSYNC();
+        return -1;
+    }
+    bp_ring_state(J, w, r, g);
     WSYNC();
     return fl & FL_ERR;
 }
@@ -2300,8 +2576,16 @@ __device__ __forceinline__ uint32_t step_env(
     if (done && autoreset) {                                                // reset() without a seed
         if constexpr (INLINE_GEN) {
             if (autoreset == 1) {
-                if constexpr (SBNB > 0) flags |= sb_generate<SBNB, CODD, TMG_SB_VDET_STEP != 0>(P, w, lane, J, g, cl);
-                else flags |= generate_board(P, w, lane, J, g, cl);
+                int fg = -1;
+                if constexpr (SBNB > 0 && !TMG_BP) {
+                    fg = sb_generate<SBNB, CODD, TMG_SB_VDET_STEP != 0>(P, w, lane, J, g, cl);
+                } else if constexpr (SBNB > 0) {
+                    if (P.C <= 32) fg = bp_generate<SBNB>(P, w, lane, J, g);
+                    if (fg < 0) fg = sb_generate_exact<SBNB, CODD>(P, w, lane, J, g, cl);
+                } else {
+                    fg = generate_board(P, w, lane, J, g, cl);
+                }
+                flags |= fg;
                 changed = true;
             }
         }                                      // autoreset == 2: reset_kernel regenerates FL_RESET envs next
@@ -2339,12 +2623,13 @@ __device__ __forceinline__ uint32_t step_env(
 // TileMatchEnv.step over a batch, one wave per env.
 template <int MAXN, bool GEN, int SBNB = 0, bool CODD = false>
 __global__ __launch_bounds__(64 * TMG_WPB, MAXN == 128 ? (GEN ? TMG_GEN128_WAVES : TMG_LEAN128_WAVES) : (GEN ? TMG_GEN512_WAVES : TMG_WPE)) void step_kernel(
-    Params P, int64_t n, int8_t *__restrict__ board, uint64_t *__restrict__ rng, int32_t *__restrict__ timer,
+    Params P_, int64_t n, int8_t *__restrict__ board, uint64_t *__restrict__ rng, int32_t *__restrict__ timer,
     const int32_t *__restrict__ actions, int32_t *__restrict__ reward, int32_t *__restrict__ n_new,
     int32_t *__restrict__ n_act, uint8_t *__restrict__ flags_out, uint64_t *__restrict__ eff, int trust_eff,
     int autoreset) {
     TMG_SMEM_DECL(smem);
     using WS = Ws<MAXN, GEN>;
+    const Params &P = TMG_KERNARG_PARAMS(P_);
     const int lane = threadIdx.x & 63;
     const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
     WS &w = reinterpret_cast<WS *>(smem)[wv];
@@ -2411,10 +2696,22 @@ __device__ __forceinline__ void reset_env(const Params &P, WS &w, int lane, int6
     Rng g = load_rng(rng + e * 5);
     const LaneJump J = load_jump<MAXN, TMG_LANE_BATCH != 0>(P, lane, g);
     const Cells<MAXN / 64> cl = make_cells<MAXN / 64>(P, lane);
-    int fl;
-    if constexpr (SBNB > 0) fl = sb_generate<SBNB, CODD, TMG_SB_VDET != 0>(P, w, lane, J, g, cl);   // board.py:95-109
-    else if constexpr (MAXN > 128 && TMG_RESET_RING) fl = generate_board_ring(P, w, lane, J, g, cl);
-    else fl = generate_board<TMG_RESET_ROLL != 0, TMG_RESET_PRE != 0>(P, w, lane, J, g, cl);
+    // board.py:95-109: on row bit-planes (C <= 32); a Lemire rejection or a
+    // wider board takes the exact draw-by-draw path
+    int fl = -1;
+    if constexpr (SBNB > 0 && TMG_BP) {
+        if (P.C <= 32) fl = bp_generate<SBNB>(P, w, lane, J, g);
+    }
+    if (fl < 0) {
+        if constexpr (MAXN == 128 && SBNB > 0) {
+            if constexpr (TMG_BP) fl = sb_generate_exact<SBNB, CODD>(P, w, lane, J, g, cl);
+            else fl = sb_generate<SBNB, CODD, TMG_SB_VDET != 0>(P, w, lane, J, g, cl);
+        } else if constexpr (MAXN > 128 && !TMG_BP) {
+            fl = generate_board_ring(P, w, lane, J, g, cl);
+        } else {
+            fl = generate_board(P, w, lane, J, g, cl);
+        }
+    }
     note_status(P, lane, fl ? ST_INTERNAL : 0u);
     store_board(P, w, lane, board + e * 2 * N);
     store_rng(rng + e * 5, g, lane);
@@ -2424,12 +2721,13 @@ __device__ __forceinline__ void reset_env(const Params &P, WS &w, int lane, int6
 }
 
 template <int MAXN, int SBNB = 0, bool CODD = false>
-__global__ __launch_bounds__(64 * TMG_WPB, MAXN > 128 ? TMG_RESET512_WAVES : 1) void reset_kernel(Params P, int64_t n, int8_t *__restrict__ board,
+__global__ __launch_bounds__(64 * TMG_WPB, MAXN > 128 ? TMG_RESET512_WAVES : 1) void reset_kernel(Params P_, int64_t n, int8_t *__restrict__ board,
                                                              uint64_t *__restrict__ rng, int32_t *__restrict__ timer,
                                                              uint64_t *__restrict__ eff,
                                                              const uint8_t *__restrict__ env_mask, int mask_bits) {
     TMG_SMEM_DECL(smem);
     using WS = Ws<MAXN, false>;
+    const Params &P = TMG_KERNARG_PARAMS(P_);
     const int lane = threadIdx.x & 63;
     const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
     WS &w = reinterpret_cast<WS *>(smem)[wv];

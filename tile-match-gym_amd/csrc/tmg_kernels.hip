@@ -93,7 +93,13 @@ void launch_step512(bool gen, dim3 grid, hipStream_t s, const Params &P, const S
 
 void launch_reset512(dim3 grid, hipStream_t s, const Params &P, int64_t n, int8_t *board, uint64_t *rng,
                      int32_t *timer, uint64_t *eff, const uint8_t *env_mask, int mask_bits) {
-    reset_one<512, 0, false>(grid, s, P, n, board, rng, timer, eff, env_mask, mask_bits);
+    // NB = colour bit-planes of the row-plane generate (bp_generate)
+    switch (sb_planes(P.k)) {
+    case 1: reset_one<512, 1, false>(grid, s, P, n, board, rng, timer, eff, env_mask, mask_bits); break;
+    case 2: reset_one<512, 2, false>(grid, s, P, n, board, rng, timer, eff, env_mask, mask_bits); break;
+    case 3: reset_one<512, 3, false>(grid, s, P, n, board, rng, timer, eff, env_mask, mask_bits); break;
+    default: reset_one<512, 4, false>(grid, s, P, n, board, rng, timer, eff, env_mask, mask_bits); break;
+    }
 }
 void launch_effective512(dim3 grid, hipStream_t s, const Params &P, int64_t n, const int8_t *board, uint64_t *eff) {
     effective_one<512>(grid, s, P, n, board, eff);

@@ -446,7 +446,7 @@ __device__ __forceinline__ void sb_draw_rows(const Params &P, WS &w, int lane, c
 // VDET: the line search on the lane codes (sb_first_line_key_v) instead of
 // the bitboards.  Used by reset_kernel only: in the lean step kernel it costs
 // registers on the normal-step path (A/B).
-template <int NB, bool CODD, bool VDET = false, class WS>
+template <int NB, bool CODD, bool VDET = false, bool GEN = false, class WS>
 __device__ __forceinline__ int sb_ensure(const Params &P, WS &w, int lane, const LaneJump &J, Rng &g,
                                          const Cells<WS::NP> &cl, SBC &c, bool dirty, bool clean) {
     int keyA, keyB;
@@ -488,7 +488,7 @@ __device__ __forceinline__ int sb_ensure(const Params &P, WS &w, int lane, const
         }
         if (scan_effective_clean<false>(P, w, lane)) break;   // types all 1, no line
         if (shuffles >= TMG_MAX_SHUFFLES) { fl |= FL_ERR; break; }
-        COVER(CV_SHUFFLE);
+        COVER(GEN ? CV_SHUFFLE_GEN : CV_SHUFFLE);
         WSYNC();
         shuffle(P, w, lane, g);
         c = sb_codes_from_lds(P, w.brd, lane);
@@ -507,7 +507,7 @@ __device__ __forceinline__ int sb_generate_exact(const Params &P, WS &w, int lan
     SBC c{0, 0};
     sb_draw_rows<NB>(P, w, lane, J, g, P.R - 1, c, sb_draw_pre(J, g));
     for (int p = lane; p < P.N; p += 64) w.brd[P.N + p] = 1;
-    return sb_ensure<NB, CODD, VDET>(P, w, lane, J, g, cl, c, true, false) & FL_ERR;
+    return sb_ensure<NB, CODD, VDET, true>(P, w, lane, J, g, cl, c, true, false) & FL_ERR;
 }
 
 // rows 0..M/C-1 of the lane codes <- the ring's next M colours (ring_take for

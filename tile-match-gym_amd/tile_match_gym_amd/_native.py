@@ -32,7 +32,7 @@ STATUS_INTERNAL, STATUS_OVERFLOW, STATUS_CALLER = 1, 2, 4
 # CV_* branch counters of TMG_COVER builds (tmg_board.hip), in index order
 COVER_NAMES = ("sb_lean", "sb_normal", "sb_laser", "sb_perp_bomb", "sb_row_bomb", "sb_closure", "sb_fallback",
                "lds_normal", "lds_laser", "lds_bomb", "lds_fallback", "serial_step", "serial_act", "serial_cookie",
-               "combo", "spill", "spill_run", "shuffle", "reject", "fast")
+               "combo", "spill", "spill_run", "shuffle", "reject", "fast", "shuffle_gen", "reject_gen")
 
 SPECIAL_BITS = {"cookie": 1, "vertical_laser": 2, "horizontal_laser": 4, "bomb": 8}
 FLAG_DONE, FLAG_COMBO, FLAG_SHUFFLED, FLAG_RESET, FLAG_OVERFLOW, FLAG_ERROR = 1, 2, 4, 8, 0x40, 0x80

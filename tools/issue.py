@@ -60,7 +60,8 @@ def main():
                 continue
             for c, v in rows[i].items():
                 tot[c] += v
-        env_steps = steps * bench.CONFIGS[cfg][5]
+        boards = int(os.environ.get("BOARDS", "0")) or bench.CONFIGS[cfg][5]   # bench --boards of the profiled runs
+        env_steps = steps * boards
         out[cfg] = {
             "valu_per_env_step": round(tot["SQ_INSTS_VALU"] / env_steps, 2),
             "salu_per_env_step": round(tot["SQ_INSTS_SALU"] / env_steps, 2),
@@ -68,6 +69,9 @@ def main():
             "smem_per_env_step": round(tot["SQ_INSTS_SMEM"] / env_steps, 2),
             "waves_per_env_step": round(tot["SQ_WAVES"] / env_steps, 4),
             "env_steps": env_steps,
+            # the bench run these counts belong to (bench.py attaches them only to a line of the same run shape)
+            "boards_per_gpu": boards,
+            "env_groups_per_gpu": int(os.environ.get("GROUPS", "3")),
             "dispatches": {"step_kernel": n_step, "reset_kernel": n_reset},
             "source": f"rocprofv3 --pmc {' '.join(COUNTERS)} --kernel-trace, bench.py --config {cfg} "
                       f"(steps + warmup = {steps}); scripts/gpu_issue.sh, tools/issue.py",

@@ -40,6 +40,8 @@ def main():
     import bench
     root = sys.argv[1]
     steps = int(sys.argv[2]) if len(sys.argv) > 2 else None
+    boards = int(os.environ.get("BOARDS", "0"))          # bench --boards of the profiled runs (0: the config's)
+    groups = int(os.environ.get("GROUPS", "3"))          # bench --groups of the profiled runs
     out = {}
     for d in sorted(glob.glob(os.path.join(root, "*_FETCH_SIZE"))):
         cfg = os.path.basename(d).split("_")[0]
@@ -57,8 +59,11 @@ def main():
             "hbm_bytes_per_env_step": (round((2 * sum(per_dispatch(d, "FETCH_SIZE", True))
                                                + sum(per_dispatch(os.path.join(root, f"{cfg}_WRITE_SIZE"),
                                                                   "WRITE_SIZE", True))) * 1024
-                                              / (steps * bench.CONFIGS[cfg][5]), 1) if steps else None),
+                                              / (steps * (boards or bench.CONFIGS[cfg][5])), 1) if steps else None),
             "correction": "FETCH_SIZE x2 (gfx950 half-count, MI355X_MICROARCH.md HBM section); WRITE_SIZE as is",
+            # the bench run these counts belong to (bench.py attaches them only to a line of the same run shape)
+            "boards_per_gpu": boards or bench.CONFIGS[cfg][5],
+            "env_groups_per_gpu": groups,
         }
     json.dump(out, sys.stdout, indent=1)
     print()

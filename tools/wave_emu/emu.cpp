@@ -290,7 +290,12 @@ static void emu_do_reset(const tmg::Params &P, int64_t n, int8_t *board, uint64_
     } else if (P.N <= 128) {
         emu_reset_kernel<128, 0, false>(P, n, board, rng, timer, eff, mask, bits);
     } else {
-        emu_reset_kernel<512, 0, false>(P, n, board, rng, timer, eff, mask, bits);
+        switch (tmg::sb_planes(P.k)) {
+        case 1: emu_reset_kernel<512, 1, false>(P, n, board, rng, timer, eff, mask, bits); break;
+        case 2: emu_reset_kernel<512, 2, false>(P, n, board, rng, timer, eff, mask, bits); break;
+        case 3: emu_reset_kernel<512, 3, false>(P, n, board, rng, timer, eff, mask, bits); break;
+        default: emu_reset_kernel<512, 4, false>(P, n, board, rng, timer, eff, mask, bits); break;
+        }
     }
 }
 

@@ -45,6 +45,8 @@ inline int emu_update_dpp(int old, int src, int ctrl, int row_mask, int bank_mas
 #define __builtin_amdgcn_ds_bpermute(a, v) ((int)emu_readlane((uint32_t)(v), ((a) >> 2) & 63))
 #define __builtin_amdgcn_alignbyte(a, b, s) \
     ((uint32_t)(((((uint64_t)(uint32_t)(a)) << 32) | (uint32_t)(b)) >> (8 * ((s) & 3))))
+#define __builtin_amdgcn_alignbit(a, b, s) \
+    ((uint32_t)(((((uint64_t)(uint32_t)(a)) << 32) | (uint32_t)(b)) >> ((s) & 31)))
 #define __builtin_amdgcn_fence(order, scope) emu_sync()
 #define __builtin_amdgcn_wave_barrier() ((void)0)
 inline void __syncthreads() { emu_sync(); }
@@ -52,6 +54,9 @@ inline int __popcll(uint64_t x) { return __builtin_popcountll(x); }
 inline int __clzll(uint64_t x) { return x ? __builtin_clzll(x) : 64; }
 inline int __ffsll(unsigned long long x) { return __builtin_ffsll((long long)x); }
 inline uint64_t __umul64hi(uint64_t a, uint64_t b) { return (uint64_t)(((unsigned __int128)a * b) >> 64); }
+
+struct alignas(16) uint4 { uint32_t x, y, z, w; };
+inline uint4 make_uint4(uint32_t x, uint32_t y, uint32_t z, uint32_t w) { return uint4{x, y, z, w}; }
 
 inline int min(int a, int b) { return a < b ? a : b; }
 inline int max(int a, int b) { return a > b ? a : b; }
@@ -79,3 +84,4 @@ inline unsigned emu_mbcnt_hi(unsigned m, unsigned acc) {
 #define TMG_KEEP_V3(x, y, z) ((void)0)
 #define TMG_KEEP_V(x) ((void)0)
 #define TMG_SMEM_DECL(name) unsigned char *name = emu_smem()
+#define TMG_KERNARG_PARAMS(p) (p)
