@@ -21,16 +21,15 @@ struct U128 {
 };
 
 __host__ __device__ __forceinline__ U128 mul128(U128 a, U128 b) {   // low 128 bits of a*b
-#ifndef TMG_MUL128_HAND
-#define TMG_MUL128_HAND 1      // 0: the compiler's 64-bit lowering (A/B: c2 7.26 vs 7.30, c5 1.20 vs 1.24 x 10^8)
-#endif
-#if defined(__HIP_DEVICE_COMPILE__) && TMG_MUL128_HAND
+#if defined(__HIP_DEVICE_COMPILE__)
     // The ten 32x32 partial products below 2^128 (the compiler's 64-bit
     // lowering of lo*lo, umulhi and the two cross terms issues thirteen): six
     // 32x32+64 multiply-adds (v_mad_u64_u32) for the terms whose high halves
     // matter, four 32-bit products for the ones that land at bits 96..127.
     // Integer multiplies issue at ~1/1.7 the rate of a 32-bit add on gfx950
-    // (tools/mul_probe.hip), and the PCG64 jump-ahead is most of a redraw's VALU.
+    // (tools/mul_probe.hip), and the PCG64 jump-ahead is most of a redraw's VALU
+    // (A/B against the compiler's 64-bit lowering: c2 7.30 vs 7.26, c5 1.24 vs
+    // 1.20 x 10^8).
     const uint32_t a0 = (uint32_t)a.lo, a1 = (uint32_t)(a.lo >> 32), a2 = (uint32_t)a.hi, a3 = (uint32_t)(a.hi >> 32);
     const uint32_t b0 = (uint32_t)b.lo, b1 = (uint32_t)(b.lo >> 32), b2 = (uint32_t)b.hi, b3 = (uint32_t)(b.hi >> 32);
     const uint64_t p00 = (uint64_t)a0 * b0;
@@ -41,9 +40,6 @@ __host__ __device__ __forceinline__ U128 mul128(U128 a, U128 b) {   // low 128 b
     hi = (uint64_t)a2 * b0 + hi;
     hi += (p10 >> 32) + ((uint64_t)(a0 * b3 + a1 * b2 + a2 * b1 + a3 * b0) << 32);
     return U128{(p10 << 32) | (uint32_t)p00, hi};
-#elif defined(__HIP_DEVICE_COMPILE__)
-    uint64_t hi = __umul64hi(a.lo, b.lo) + a.lo * b.hi + a.hi * b.lo;
-    return U128{a.lo * b.lo, hi};
 #else
     uint64_t hi = (uint64_t)(((unsigned __int128)a.lo * b.lo) >> 64) + a.lo * b.hi + a.hi * b.lo;
     return U128{a.lo * b.lo, hi};

@@ -22,78 +22,17 @@
 
 namespace tmg {
 
-#ifndef TMG_WPB
-#define TMG_WPB 1          // waves (boards) per workgroup
-#endif
-#ifndef TMG_WPE
-#define TMG_WPE 0          // minimum waves per SIMD requested from the register allocator (0 = compiler's choice)
-#endif
-#if TMG_WPE > 0
-#define TMG_LAUNCH_BOUNDS __launch_bounds__(64 * TMG_WPB, TMG_WPE)
-#else
-#define TMG_LAUNCH_BOUNDS __launch_bounds__(64 * TMG_WPB)
-#endif
-
-#if TMG_WPB == 1
+// One wave (one board) per 64-thread workgroup: a workgroup's slot is held
+// until its slowest wave ends, so 2 / 4 boards per workgroup measured slower
+// (DESIGN.md §7).  The wave synchronises its LDS accesses with the workgroup
+// barrier.
 #define WSYNC() __syncthreads()
-#else
-#define WSYNC()                                                  \
-    do {                                                         \
-        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");   \
-        __builtin_amdgcn_wave_barrier();                         \
-    } while (0)
-#endif
-#ifndef TMG_XCD
-#define TMG_XCD 1          // XCD-aware workgroup -> env mapping
-#endif
 
-#ifndef TMG_LEAN_DEFER
-#define TMG_LEAN_DEFER 0       // 1: 128-cell lean step kernels autoreset by a masked reset launch (A/B: -1 %)
-#endif
-#ifndef TMG_STATUS
-#define TMG_STATUS 1           // 0: no sticky status word (A/B of its cost only; tmg_status then reads 0)
-#endif
-#ifndef TMG_GEN128_WAVES
-#define TMG_GEN128_WAVES 5     // min waves per SIMD for the 128-cell general step kernel (caps it at 96 VGPRs)
-#endif
-#ifndef TMG_RESET_ROLL
-#define TMG_RESET_ROLL 0       // 1: the 512-cell reset kernel's line search as a rolled loop (fewer VGPRs)
-#endif
-#ifndef TMG_RESET_PRE
-#define TMG_RESET_PRE 1        // the 512-cell reset kernel evaluates each redraw's first PCG batch before its line search
-#endif
-#ifndef TMG_GEN512_WAVES
-#define TMG_GEN512_WAVES TMG_WPE   // min waves per SIMD for the 512-cell general step kernel (0: compiler's choice, 3)
-#endif
-#ifndef TMG_LEAN128_WAVES
-#define TMG_LEAN128_WAVES TMG_WPE   // min waves per SIMD for the <= 128-cell lean step kernels (c2)
-#endif
-#ifndef TMG_RQ128_WAVES
-#define TMG_RQ128_WAVES 5      // min waves per SIMD for the 128-cell reset-queue kernel (87 VGPRs, no spill)
-#endif
-#ifndef TMG_RESET_RECOMP
-// 512-cell reset kernel: 1 rebuilds the byte line search's cell geometry per
-// pass (for C % 4 != 0; C % 4 == 0 takes first_line_row_dw) instead of keeping
-// it in VGPRs: 80 VGPRs, 6 waves/SIMD.  With the colour ring and the dword
-// search: c5 1.29 x 10^8 (0 at 5 waves/SIMD: 1.24; dword search off at
-// 5 waves/SIMD: 1.28)
-#define TMG_RESET_RECOMP 1
-#endif
-#ifndef TMG_CELLS_ONCE
-#define TMG_CELLS_ONCE 1       // 512-cell board_move: cell geometry computed once per step (1) or rebuilt where used (0; c5 neutral)
-#endif
-#ifndef TMG_RING_DWSEARCH
-#define TMG_RING_DWSEARCH 1    // 512-cell generate: remove_colour_lines' line search over dwords when C % 4 == 0
-#endif
-#ifndef TMG_RESET_RING
-#define TMG_RESET_RING 1       // 512-cell reset kernel: generate_board's colours through the LDS colour ring
-#endif
-#ifndef TMG_PREFETCH
-#define TMG_PREFETCH 1         // step prologue loads issued before the action is known (step_env)
-#endif
-#ifndef TMG_RESET512_WAVES
-#define TMG_RESET512_WAVES 6   // min waves per SIMD for the 512-cell reset kernel (caps its VGPRs; see TMG_RESET_RECOMP)
-#endif
+// Minimum waves per SIMD asked of the register allocator (launch bounds), per
+// kernel; each measured on the MI355X against its neighbours.
+constexpr int kLean128Waves = 7;     // step_kernel<128, false>: the c2 / c4 kernel (72 VGPRs)
+constexpr int kGen128Waves = 5;      // step_kernel<128, true>: c3 (96 VGPRs; 6 / 7 spill and lose)
+constexpr int kReset512Waves = 7;    // reset_kernel<512>: c5's regeneration (62 VGPRs: 8 waves)
 
 // compiler-only ordering point between a wave's LDS loads and later stores
 #define WFENCE() __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront")
@@ -122,16 +61,12 @@ enum : uint32_t { ST_INTERNAL = 1, ST_OVERFLOW = 2, ST_CALLER = 4 };
 // shuffle part can spin forever on a colour multiset that has no playable
 // line-free arrangement (e.g. 3x3 with at most two tiles of each colour): there
 // the reference loops forever; here the wave ends the loop with FL_ERR.
-#ifndef TMG_MAX_SHUFFLES
-#define TMG_MAX_SHUFFLES (1 << 12)   // shuffles per loop
-#endif
+constexpr int kMaxShuffles = 1 << 12;   // shuffles per loop
 
 // Per-stream queue of the envs whose step ran out of LDS list space
 // (step_env), drained by spill_kernel.  Sized by the host for the envs of
 // the launch (cap >= n), so every such env fits: no step is ever dropped.
-#ifndef TMG_SPILL_WAVES
-#define TMG_SPILL_WAVES 16       // spill_kernel workgroups (one wave, one WsSerialBig each)
-#endif
+constexpr int kSpillWaves = 16;          // spill_kernel workgroups (one wave, one WsSerialBig each)
 struct SpillQ {
     uint32_t count, done;        // queued envs; spill_kernel waves finished
     unsigned long long total;    // envs re-run so far (diagnostic, tmg_spills)
@@ -202,9 +137,8 @@ struct Params {
     int oh_dtype, oh_ch, oh_nsel; // TMG_DTYPE_*; channels = k + nsel
     uint32_t oh_sel;              // type ids of the special channels, int8 each (wrappers.py:37-46)
     SpillQ *spill;                // this launch's stream's spill queue (general kernels)
-    void *spill_ws;               // TMG_SPILL_WAVES WsSerialBig<MAXN> for spill_kernel
+    void *spill_ws;               // kSpillWaves WsSerialBig<MAXN> for spill_kernel
     unsigned long long *cover;    // TMG_COVER builds: CV_COUNT hit counters (null otherwise)
-    uint64_t *stamps;             // TMG_STAMPS builds: per-env phase stamps (null otherwise)
 };
 
 // The kernels take Params by value as their FIRST argument and read it
@@ -212,11 +146,8 @@ struct Params {
 // Used as a by-value argument, the whole block is loaded into SGPRs in the
 // entry block (AMDGPULowerKernelArguments) and spilled to VGPR lanes before
 // anything else runs, e.g. before the ineffective-move exit of a step.
-#ifndef TMG_KARG
-#define TMG_KARG 1             // A/B only (0: Params used as the by-value argument)
-#endif
 #ifndef TMG_KERNARG_PARAMS
-#if defined(__HIP_DEVICE_COMPILE__) && TMG_KARG
+#if defined(__HIP_DEVICE_COMPILE__)
 #define TMG_KERNARG_PARAMS(p) (*(const Params *)__builtin_amdgcn_kernarg_segment_ptr())
 #else
 #define TMG_KERNARG_PARAMS(p) (p)          // the host pass of the kernel templates (never executed)
@@ -253,7 +184,6 @@ inline Params make_params(int R, int C, int k, int smask, int num_moves, const u
     P.spill = nullptr;
     P.spill_ws = nullptr;
     P.cover = nullptr;
-    P.stamps = nullptr;
     P.oh = nullptr;
     P.oh_dtype = P.oh_ch = P.oh_nsel = 0;
     P.oh_sel = 0;
@@ -279,38 +209,15 @@ inline Params make_params(int R, int C, int k, int smask, int num_moves, const u
 __device__ __forceinline__ int div_c(const Params &P, int x) { return (int)(((uint32_t)x * P.cmag) >> 20); }
 __device__ __forceinline__ int div_cm1(const Params &P, int x) { return (int)(((uint32_t)x * P.cm1mag) >> 20); }
 
-// Diagnostic build only (TMG_STAMPS=1, never the product library): lane 0
-// records s_memrealtime (100 MHz) at phase boundaries of every env.
-#ifndef TMG_STAMPS
-#define TMG_STAMPS 0
-#endif
-#if TMG_STAMPS
-constexpr int kStampEnvs = 1 << 18, kStampSlots = 8;
-#define STAMP(e, slot)                                                                           \
-    do {                                                                                         \
-        if (lane == 0 && P.stamps && (e) < kStampEnvs) P.stamps[(e) * kStampSlots + (slot)] = __builtin_amdgcn_s_memrealtime(); \
-    } while (0)
-#define STAMPV(e, slot, v)                                                                       \
-    do {                                                                                         \
-        if (lane == 0 && P.stamps && (e) < kStampEnvs) P.stamps[(e) * kStampSlots + (slot)] = (uint64_t)(v); \
-    } while (0)
-#else
-#define STAMP(e, slot) ((void)0)
-#define STAMPV(e, slot, v) ((void)0)
-#endif
 
-// Workgroup -> first env.  The dispatcher hands workgroup b to XCD b % 8; with
-// TMG_XCD the host pads the grid to a multiple of 8 and XCD x gets the
-// contiguous env block [x*G/8, (x+1)*G/8), so the per-env arrays (actions,
-// timer, outputs, masks) are touched by one XCD's L2 per cache line instead
-// of eight (speed only: correctness never depends on the placement).
-__device__ __forceinline__ int64_t wg_env0() {
-#if TMG_XCD
+// Workgroup -> env.  The dispatcher hands workgroup b to XCD b % 8; the host
+// pads the grid to a multiple of 8 and XCD x gets the contiguous env block
+// [x*G/8, (x+1)*G/8), so the per-env arrays (actions, timer, outputs, masks)
+// are touched by one XCD's L2 per cache line instead of eight (speed only:
+// correctness never depends on the placement).
+__device__ __forceinline__ int64_t wg_env() {
     const int64_t per = gridDim.x >> 3;
-    return ((int64_t)(blockIdx.x & 7) * per + (blockIdx.x >> 3)) * TMG_WPB;
-#else
-    return (int64_t)blockIdx.x * TMG_WPB;
-#endif
+    return (int64_t)(blockIdx.x & 7) * per + (blockIdx.x >> 3);
 }
 
 // scalar slots in LDS (lane-0 sections publish through these)
@@ -368,13 +275,9 @@ struct ListStore {
 // the general 20x20 kernel fits twice the waves per CU in LDS.  A step that
 // runs out (FL_OVF from the list machinery) is not written back: the env goes
 // to the spill queue and spill_kernel re-runs the step on WsSerialBig.
-#ifndef TMG_CAP128
-#define TMG_CAP128 64         // lane-0 list capacity of the <= 128-cell general kernels (cells; more spills)
-#endif
-#ifndef TMG_CAP512
-#define TMG_CAP512 128        // lane-0 list capacity of the 512-cell general kernels (cells; overflow -> spill path)
-#endif
-template <int MAXN, int CAP = (MAXN > 128 ? TMG_CAP512 : TMG_CAP128)>
+constexpr int kCap128 = 64;              // lane-0 list capacity of the <= 128-cell general kernels (cells)
+constexpr int kCap512 = 128;             // lane-0 list capacity of the 512-cell general kernels (cells)
+template <int MAXN, int CAP = (MAXN > 128 ? kCap512 : kCap128)>
 using WsSerial = ListStore<4 * CAP + 256, CAP + 64, 2 * CAP + 64, CAP + 32, 4 * CAP + 256, CAP + 8>;
 
 // Global-memory lists sized at the worst case of any board of <= MAXN cells
@@ -466,17 +369,7 @@ __device__ __forceinline__ void rng_bcast(Rng &g) {
 
 struct LaneJump {
     U128 Aj, Gj, incG;    // A^{lane+1}, G_{lane+1}, G_{lane+1} * inc
-    // wave-uniform (512-cell kernels): A^64 and G_64 * inc, so a lane steps its
-    // own state one batch of 64 outputs further, s' = A^64 s + G_64 inc, with
-    // no cross-lane dependency (TMG_LANE_BATCH)
-    U128 A64, incG64;
 };
-#ifndef TMG_LANE_BATCH
-#define TMG_LANE_BATCH 0         // 512-cell reset kernel (1: measured slower, c5 1.12 vs 1.15 x 10^8)
-#endif
-#ifndef TMG_LANE_BATCH_STEP
-#define TMG_LANE_BATCH_STEP 0    // 512-cell step kernels (+5 VGPRs: 3 -> 2 waves/SIMD for the general one)
-#endif
 
 // single-lane stream (serial replays, shuffle)
 __device__ __forceinline__ uint64_t r_next64(Rng &g) {
@@ -510,15 +403,10 @@ __device__ __forceinline__ uint32_t r_interval(Rng &g, uint32_t max) {     // ra
 
 // dst[0..M) <- Generator.integers(1, k+1, M) (board.py:97,129,239), lane-parallel:
 // lane j evaluates PCG output j of the batch by jump-ahead; the caller syncs.
-// pre: the batch's first 64 outputs already evaluated (jump-ahead from g), or null
 // ONE: M <= 128, i.e. one batch of 64 outputs (no loop-carried state)
-struct DrawPre {
-    U128 sj;
-    uint64_t out;
-};
 template <bool ONE = false, class T>
 __device__ __forceinline__ void draw_colours(const Params &P, int lane, const LaneJump &J, Rng &g, int M, T *dst,
-                                             int8_t *trash, const DrawPre *pre = nullptr) {
+                                             int8_t *trash) {
     if (M <= 0) return;
     const uint32_t k = (uint32_t)P.k;
     if (k == 1) {                                          // rng == 0: numpy draws nothing
@@ -541,16 +429,8 @@ __device__ __forceinline__ void draw_colours(const Params &P, int lane, const La
     U128 sj{0, 0};
     uint64_t out = 0;
     for (int base = 0; base < n64; base += 64) {
-        if (pre && base == 0) {
-            sj = pre->sj;
-            out = pre->out;
-        } else if (!ONE && base > 0 && (J.A64.lo | J.A64.hi) != 0) {   // load_jump<.., LB>
-            sj = add128(mul128(sj, J.A64), J.incG64);               // the previous batch was a full 64
-            out = xsl_rr(sj);
-        } else {
-            sj = add128(mul128(J.Aj, s), J.incG);
-            out = xsl_rr(sj);
-        }
+        sj = add128(mul128(J.Aj, s), J.incG);
+        out = xsl_rr(sj);
         const int j = base + lane;
         const uint64_t m0 = (uint64_t)(uint32_t)out * k, m1 = (out >> 32) * k;
         const bool ok0 = j < n64, ok1 = 2 * j + 1 < need;          // ok1 implies ok0
@@ -560,11 +440,9 @@ __device__ __forceinline__ void draw_colours(const Params &P, int lane, const La
         *d1 = (T)(1 + (m1 >> 32));
         rej |= (ok0 & ((uint32_t)m0 < P.thr)) | (ok1 & ((uint32_t)m1 < P.thr));
         const int cnt = n64 - base < 64 ? n64 - base : 64;
-        if (ONE || (J.A64.lo | J.A64.hi) == 0 || base + 64 >= n64) {   // the stream position after the batch
-            s.lo = rdlane64(sj.lo, cnt - 1);
-            s.hi = rdlane64(sj.hi, cnt - 1);
-            last_hi = rdlane64(out >> 32, cnt - 1);
-        }
+        s.lo = rdlane64(sj.lo, cnt - 1);                   // the stream position after the batch
+        s.hi = rdlane64(sj.hi, cnt - 1);
+        last_hi = rdlane64(out >> 32, cnt - 1);
         if constexpr (ONE) break;
     }
     if (P.thr != 0u && __ballot(rej) != 0ULL) {            // Lemire rejection: exact serial replay
@@ -631,38 +509,6 @@ __device__ __forceinline__ void load_board(const Params &P, WS &w, int lane, con
         for (int i = lane; i < nb; i += 64) w.brd[i] = src[i];
     }
 }
-// An env's board read into registers at the top of a step, before the
-// effectiveness test decides whether it is needed (one dword per lane and
-// 64-dword pass; boards with an odd cell count are not dword-aligned in HBM
-// and take load_board instead).
-template <int MAXN>
-struct BoardPre {
-    static constexpr int K = (2 * MAXN / 4 + 63) / 64;
-    uint32_t v[K];
-};
-template <int MAXN>
-__device__ __forceinline__ void board_prefetch(const Params &P, BoardPre<MAXN> &b, int lane, const int8_t *src) {
-    const int nw = (2 * P.N) >> 2;
-    const uint32_t *s = reinterpret_cast<const uint32_t *>(src);
-#pragma unroll
-    for (int k = 0; k < BoardPre<MAXN>::K; k++) {
-        const int i = k * 64 + lane;
-        b.v[k] = (!(P.N & 1) && i < nw) ? s[i] : 0u;
-    }
-}
-template <int MAXN, class WS>
-__device__ __forceinline__ void board_from_prefetch(const Params &P, WS &w, const BoardPre<MAXN> &b, int lane,
-                                                    const int8_t *src) {
-    if (P.N & 1) { load_board(P, w, lane, src); return; }
-    const int nw = (2 * P.N) >> 2;
-    uint32_t *d = reinterpret_cast<uint32_t *>(w.brd);
-#pragma unroll
-    for (int k = 0; k < BoardPre<MAXN>::K; k++) {
-        const int i = k * 64 + lane;
-        if (i < nw) d[i] = b.v[k];
-    }
-}
-
 template <class WS>
 __device__ __forceinline__ void store_board(const Params &P, const WS &w, int lane, int8_t *dst) {
     const int nb = 2 * P.N;
@@ -931,30 +777,7 @@ __device__ __forceinline__ int first_line_row(const Params &P, const WS &w, int 
     const int8_t *col = w.brd, *typ = w.brd + N;
     const int last = min((lim + 1) * C, N) - 1;          // highest cell that may anchor a line
     int best = -1, stop = -2;                            // stop: lowest pass still to scan, once found
-    if constexpr (!ROLL && WS::NP > 2 && TMG_RESET_RECOMP) {
-        // 512-cell reset kernel: unrolled (the passes' loads overlap), the cell
-        // geometry of each scanned pass rebuilt from an opaque lane index
-        // instead of eight per-pass VGPRs kept across the redraw loop
-        (void)cl;
-        const int ln = loop_lane(lane);
-#pragma unroll
-        for (int i = WS::NP - 1; i >= 0; i--) {
-            if (i * 64 > last || i < stop) continue;     // wave-uniform
-            const int p = i * 64 + ln;
-            const int pc = min(p, N1);
-            const int r = div_c(P, p), c = p - r * C;
-            const int x = col[pc];
-            const int u1 = col[max(pc - C, 0)], u2 = col[max(pc - 2 * C, 0)];
-            const int h1 = col[min(pc + 1, N1)], h2 = col[min(pc + 2, N1)];
-            const uint32_t tbad = ALL1 ? 0u : (uint32_t)((int)typ[pc] - 1) >> 31;
-            const uint32_t vbad = (p < N && r >= 2) ? 0u : 1u, hbad = (p < N && c + 2 < C) ? 0u : 1u;
-            const uint32_t vb = vbad | tbad | ne(u1, x) | ne(u2, x);
-            const uint32_t hb = hbad | tbad | ne(h1, x) | ne(h2, x);
-            const int base = (((r & 63) << 8) | (255 - (c & 255))) << 1;
-            best = max(best, max(vb == 0 ? base | 1 : -1, hb == 0 ? base : -1));
-            if (stop == -2 && __ballot(best >= 0) != 0ULL) stop = i - 1;
-        }
-    } else if constexpr (!ROLL || WS::NP <= 2) {
+    if constexpr (!ROLL || WS::NP <= 2) {
 #pragma unroll
         for (int i = WS::NP - 1; i >= 0; i--) {
             if (i * 64 > last || i < stop) continue;     // wave-uniform
@@ -1000,53 +823,6 @@ __device__ __forceinline__ int first_line_row(const Params &P, const WS &w, int 
     if (!(key & 1)) return rs;                            // horizontal line at (rs, c0..)
     const int c0 = 255 - ((key >> 1) & 255);
     return run_top(P, w, lane, rs, c0);                   // vertical: starts at the top of its run
-}
-
-// first_line_row for generate_board's boards (every type 1) when C % 4 == 0:
-// a lane takes one dword of the LDS colour plane, four cells of one row, so a
-// pass covers 256 cells.  The anchor tests of get_colour_lines
-// (board.py:163-193) become byte-wise: the dword against its funnel shifts by
-// one and two cells (horizontal) and against the dwords one and two rows up
-// (vertical); a zero byte of (x ^ y) | (x ^ z) is a triple (colours < 0x80, so
-// 0x80 - byte never borrows).  The lane's key is its leftmost anchor's, as in
-// first_line_row; passes are scanned bottom-up and stop one pass above the
-// first one holding an anchor.
-template <class WS>
-__device__ __forceinline__ int first_line_row_dw(const Params &P, const WS &w, int lane, int lim, int &ra) {
-    const int C = P.C, N = P.N, C4 = P.C >> 2, ND = P.N >> 2;
-    const uint32_t *b32 = reinterpret_cast<const uint32_t *>(w.brd);
-    const int last = min((lim + 1) * C, N) - 1;
-    const int ln = loop_lane(lane);
-    int best = -1, stop = -2;
-#pragma unroll
-    for (int i = (WS::MAXN / 4 + 63) / 64 - 1; i >= 0; i--) {
-        if (i * 256 > last || i < stop) continue;                       // wave-uniform
-        const int d = i * 64 + ln;
-        const bool in = d < ND;
-        const int dc = in ? d : 0;
-        const int r = div_c(P, 4 * dc), c0 = 4 * dc - r * C;
-        const uint32_t x = b32[dc], nx = b32[min(dc + 1, ND - 1)];
-        const uint32_t u1 = b32[max(dc - C4, 0)], u2 = b32[max(dc - 2 * C4, 0)];
-        const uint32_t n1 = __builtin_amdgcn_alignbyte(nx, x, 1u), n2 = __builtin_amdgcn_alignbyte(nx, x, 2u);
-        const uint32_t h = (x ^ n1) | (x ^ n2), v = (x ^ u1) | (x ^ u2);
-        const int hc = C - 2 - c0;                                      // cells of the dword that may start a run
-        const uint32_t hm = !in || hc <= 0 ? 0u : hc >= 4 ? 0x80808080u : 0x80808080u & ((1u << (8 * hc)) - 1u);
-        const uint32_t vm = in && r >= 2 ? 0x80808080u : 0u;
-        const uint32_t zh = (0x80808080u - h) & hm, zv = (0x80808080u - v) & vm;
-        const uint32_t any = zh | zv;
-        const int bi = (int)__builtin_ctz(any | 0x80000000u) >> 3;      // leftmost anchor byte
-        const int isv = (int)((zv >> (8 * bi + 7)) & 1u);
-        const int key = (((r & 63) << 8) | (255 - ((c0 + bi) & 255))) << 1 | isv;
-        best = max(best, any ? key : -1);
-        if (stop == -2 && __ballot(best >= 0) != 0ULL) stop = i - 1;
-    }
-    if (stop == -2) return -1;
-    const int key = wave_max(best);
-    const int rs = key >> 9;
-    ra = rs;
-    if (!(key & 1)) return rs;                                          // horizontal line at (rs, c0..)
-    const int c0 = 255 - ((key >> 1) & 255);
-    return run_top(P, w, lane, rs, c0);                                 // vertical: starts at the top of its run
 }
 
 // gravity, board.py:217-229 — stable partition of each column (empties to
@@ -1149,10 +925,8 @@ __device__ __forceinline__ void shuffle(const Params &P, WS &w, int lane, Rng &g
 // when the shuffle cap ended the loop.
 // noline: the board is known to hold no line (the cascade loop just found
 // none), so the first line search is skipped.
-// PRE: the next redraw's first 64 PCG outputs are evaluated before the line
-// search (they depend only on the stream position), so the jump-ahead's VALU
-// chain issues beside the search's LDS reads.
-template <bool ROLL = true, bool PRE = false, bool ALL1 = false, bool GEN = false, class WS>
+// GEN: the loop of generate_board (the cover counters tell the two apart).
+template <bool ROLL = true, bool ALL1 = false, bool GEN = false, class WS>
 __device__ __forceinline__ int ensure_playable(const Params &P, WS &w, int lane, const LaneJump &J, Rng &g,
                                 const Cells<WS::NP> &cl, bool noline = false) {
     int fl = 0;
@@ -1161,24 +935,18 @@ __device__ __forceinline__ int ensure_playable(const Params &P, WS &w, int lane,
         // > row + 2 unchanged, so after it no anchor lies below max(row + 2, ra).
         int lim = P.R - 1;
         for (; !noline;) {
-            DrawPre pre;
-            if constexpr (PRE) {
-                pre.sj = add128(mul128(J.Aj, U128{g.slo, g.shi}), J.incG);
-                pre.out = xsl_rr(pre.sj);
-                asm volatile("" ::"v"(pre.sj.lo), "v"(pre.sj.hi), "v"(pre.out));   // evaluate above the search
-            }
             int ra = 0;
             int r0 = first_line_row<ROLL, ALL1>(P, w, lane, cl, lim, ra);
             if (r0 < 0) break;
             int row = P.R - 1 < r0 + 1 ? P.R - 1 : r0 + 1;   // colour plane only, rows 0..row
-            draw_colours(P, lane, J, g, (row + 1) * P.C, w.brd, w.trash, PRE ? &pre : nullptr);
+            draw_colours(P, lane, J, g, (row + 1) * P.C, w.brd, w.trash);
             WSYNC();
             lim = min(P.R - 1, max(row + 2, ra));
         }
         // generate_board's boards (ALL1: every type 1, no cookie) are line-free
         // here, so the scan needs no precheck
         if (scan_effective(P, w, lane, cl, ALL1 || (P.smask & SP_COOKIE) == 0)) break;
-        if (shuffles >= TMG_MAX_SHUFFLES) return fl | FL_ERR;
+        if (shuffles >= kMaxShuffles) return fl | FL_ERR;
         COVER(GEN ? CV_SHUFFLE_GEN : CV_SHUFFLE);
         WSYNC();
         shuffle(P, w, lane, g);
@@ -1189,161 +957,16 @@ __device__ __forceinline__ int ensure_playable(const Params &P, WS &w, int lane,
     return fl;
 }
 
-// generate_board, board.py:95-109; returns FL_ERR when a safety cap was hit
-template <bool ROLL = true, bool PRE = false, class WS>
+// generate_board, board.py:95-109, draw by draw (boards of C > 32 columns and
+// the exact redo after a Lemire rejection; bp_generate otherwise); returns
+// FL_ERR when a safety cap was hit
+template <bool ROLL = true, class WS>
 __device__ __forceinline__ int generate_board(const Params &P, WS &w, int lane, const LaneJump &J, Rng &g, const Cells<WS::NP> &cl) {
     const int N = P.N;
     draw_colours(P, lane, J, g, N, w.brd, w.trash);
     for (int p = lane; p < N; p += 64) w.brd[N + p] = 1;
     WSYNC();
-    return ensure_playable<ROLL, PRE, true, true>(P, w, lane, J, g, cl) & FL_ERR;   // types all 1
-}
-
-// ---------------------------------------------------------------- colour ring
-// generate_board's colours (board.py:97, 129) are one sequence: every
-// Generator.integers(1, k+1, M) call takes the next M accepted 32-bit words of
-// the env's PCG64 stream (half-word buffer included), whatever M is.  The
-// 512-cell reset kernel therefore fills an LDS ring with that sequence, 64
-// outputs (128 colours) per batch, and each redraw takes its (row+1)*C
-// colours from it: every PCG64 jump-ahead then yields 128 used colours, where
-// a redraw of its own rounds its ~140 outputs up to three batches of 64.  The
-// exact stream position is recovered at the end (or before a shuffle) from the
-// latest batch's per-lane states.  A Lemire rejection anywhere in a batch
-// (Generator.integers' bounded draw, P.thr != 0) makes the caller redo the
-// board on the exact draw-by-draw path (generate_board), from the saved state.
-constexpr int kRing = 1024;                     // bytes: >= 512 cells + < 128 unconsumed
-struct ColourRing {
-    U128 fs;                                    // wave-uniform: state after the last output filled
-    U128 bs, bp;                                // wave-uniform: state before the latest / previous batch
-    int fill, cons, lbase;                      // ring indices (colours): filled, consumed, latest batch
-    int cons0;                                  // cons at ring_init: nothing taken while cons == cons0
-    bool rej;                                   // a rejected word was drawn (wave-uniform)
-};
-template <class WS>
-__device__ __forceinline__ uint8_t *ring_bytes(WS &w) { return reinterpret_cast<uint8_t *>(w.u.draw); }
-
-// The ring starting at stream position g: a buffered half-word (g.h) is the
-// first colour, at ring index 1, so every batch starts at an even index.
-template <class WS>
-__device__ __forceinline__ void ring_init(const Params &P, WS &w, int lane, const Rng &g, ColourRing &r) {
-    r.fs = U128{g.slo, g.shi};
-    r.bs = r.bp = r.fs;
-    r.fill = r.cons = 0;
-    r.lbase = 0;
-    r.rej = false;
-    if ((g.h >> 32) & 1) {
-        const uint64_t m = (uint64_t)(uint32_t)g.h * (uint32_t)P.k;
-        r.rej = (uint32_t)m < P.thr;
-        if (lane == 0) ring_bytes(w)[1] = (uint8_t)(1 + (m >> 32));
-        r.cons = 1;
-        r.fill = 2;
-    }
-    r.cons0 = r.cons;
-}
-
-template <class WS>
-__device__ __forceinline__ void ring_fill(const Params &P, WS &w, int lane, const LaneJump &J, ColourRing &r) {
-    const uint32_t k = (uint32_t)P.k;
-    const U128 sj = add128(mul128(J.Aj, r.fs), J.incG);              // output lane of the batch
-    const uint64_t out = xsl_rr(sj);
-    const uint64_t m0 = (uint64_t)(uint32_t)out * k, m1 = (out >> 32) * k;
-    const bool rj = ((uint32_t)m0 < P.thr) | ((uint32_t)m1 < P.thr);
-    if (P.thr != 0u && __ballot(rj) != 0ULL) r.rej = true;
-    uint16_t *ring = reinterpret_cast<uint16_t *>(ring_bytes(w));
-    ring[((r.fill >> 1) + lane) & (kRing / 2 - 1)] = (uint16_t)((1 + (m0 >> 32)) | ((1 + (m1 >> 32)) << 8));
-    r.bp = r.bs;
-    r.bs = r.fs;
-    r.lbase = r.fill;
-    r.fill += 128;
-    r.fs = U128{rdlane64(sj.lo, 63), rdlane64(sj.hi, 63)};
-}
-
-// dst[0..M) <- the next M colours (M <= 512; dst 4-byte aligned): whole
-// dwords, each funnel-shifted out of the two ring dwords it straddles, then the
-// M % 4 tail bytes (the cells after dst[M) are kept)
-template <class WS>
-__device__ __forceinline__ void ring_take(const Params &P, WS &w, int lane, const LaneJump &J, ColourRing &r, int M,
-                                          int8_t *dst) {
-    while (r.fill - r.cons < M) ring_fill(P, w, lane, J, r);
-    WSYNC();
-    const uint8_t *ring = ring_bytes(w);
-    const uint32_t *ring32 = reinterpret_cast<const uint32_t *>(ring);
-    uint32_t *dst32 = reinterpret_cast<uint32_t *>(dst);
-    const int nd = M >> 2, sh = r.cons & 3, q0 = r.cons >> 2;
-    for (int i = lane; i < nd; i += 64) {
-        const uint32_t lo = ring32[(q0 + i) & (kRing / 4 - 1)], hi = ring32[(q0 + i + 1) & (kRing / 4 - 1)];
-        dst32[i] = __builtin_amdgcn_alignbyte(hi, lo, (uint32_t)sh);
-    }
-    if (lane < (M & 3)) dst[(nd << 2) + lane] = (int8_t)ring[(r.cons + (nd << 2) + lane) & (kRing - 1)];
-    r.cons += M;
-}
-
-// The exact PCG64 state after the last consumed colour.  It lies in one of
-// the two latest batches: a take leaves fewer than 128 colours unconsumed, and
-// at most one batch is filled ahead of the next take.
-// The batch's per-lane states are not kept: lane L's is recomputed from the
-// batch's starting state (one jump-ahead).
-__device__ __forceinline__ void ring_state(const LaneJump &J, const ColourRing &r, Rng &g) {
-    if (r.cons == r.cons0) return;                                   // nothing taken since ring_init(g)
-    int local = r.cons - 1 - r.lbase;
-    const bool prev = local < 0;
-    local += prev ? 128 : 0;
-    const int L = local >> 1;
-    const U128 sj = add128(mul128(J.Aj, prev ? r.bp : r.bs), J.incG);
-    const U128 s{rdlane64(sj.lo, L), rdlane64(sj.hi, L)};
-    g.slo = s.lo;
-    g.shi = s.hi;
-    g.h = ((uint64_t)((local & 1) ^ 1) << 32) | (uint32_t)(xsl_rr(s) >> 32);   // lo half taken: hi half buffered
-}
-
-// generate_board (board.py:95-109) on the colour ring, for the 512-cell reset
-// kernel; the loop is ensure_playable's with the redraws taken from the ring.
-// Returns FL_ERR when a safety cap was hit; on a Lemire rejection it returns
-// generate_board's result from the unchanged starting state.
-template <class WS>
-__device__ __forceinline__ int generate_board_ring(const Params &P, WS &w, int lane, const LaneJump &J, Rng &g,
-                                                   const Cells<WS::NP> &cl) {
-    const int N = P.N;
-    const Rng g0 = g;
-    ColourRing r;
-    ring_init(P, w, lane, g, r);
-    ring_take(P, w, lane, J, r, N, w.brd);
-    for (int p = lane; p < N; p += 64) w.brd[N + p] = 1;
-    WSYNC();
-    int fl = 0;
-    for (int shuffles = 0;; shuffles++) {
-        int lim = P.R - 1;
-        for (;;) {
-            if (r.fill - r.cons < 128) ring_fill(P, w, lane, J, r);   // the next redraw's first batch, beside the search
-            int ra = 0;
-            const int r0 = (TMG_RING_DWSEARCH && !(P.C & 3)) ? first_line_row_dw(P, w, lane, lim, ra)
-                                                            : first_line_row<false, true>(P, w, lane, cl, lim, ra);
-            if (r0 < 0) break;
-            const int row = P.R - 1 < r0 + 1 ? P.R - 1 : r0 + 1;      // remove_colour_lines: rows 0..row
-            ring_take(P, w, lane, J, r, (row + 1) * P.C, w.brd);
-            WSYNC();
-            lim = min(P.R - 1, max(row + 2, ra));
-            if (r.rej) break;
-        }
-        if (r.rej) break;
-        if (scan_effective(P, w, lane, cl, true)) break;             // types all 1, line-free
-        if (shuffles >= TMG_MAX_SHUFFLES) { fl = FL_ERR; break; }
-        COVER(CV_SHUFFLE);
-        ring_state(J, r, g);                                         // shuffle draws from the stream itself
-        WSYNC();
-        shuffle(P, w, lane, g);
-        fl = FL_SHUF;
-        ring_init(P, w, lane, g, r);
-    }
-    if (r.rej) {                                                     // redo draw by draw (rare: P(reject) = thr / 2^32)
-        COVER(CV_REJECT);
-        g = g0;
-        WSYNC();
-        return generate_board<TMG_RESET_ROLL != 0, TMG_RESET_PRE != 0>(P, w, lane, J, g, cl);
-    }
-    ring_state(J, r, g);
-    WSYNC();
-    return fl & FL_ERR;
+    return ensure_playable<ROLL, true, true>(P, w, lane, J, g, cl) & FL_ERR;   // types all 1
 }
 
 // ------------------------------------------------------------ row bit-planes
@@ -1373,9 +996,6 @@ __device__ __forceinline__ int generate_board_ring(const Params &P, WS &w, int l
 // so a batch's planes are four whole dwords each, and its starting PCG64
 // state goes to one of 8 LDS slots, from which the exact stream position is
 // recovered at the end.
-#ifndef TMG_BP
-#define TMG_BP 1               // A/B only (0: the round-3 byte colour ring), removed after the measurement
-#endif
 constexpr int kBpRingDw = 32;                    // dwords per plane string (1024 colours)
 constexpr int kBpPlaneDw = 36;                   // + a guard copy of dwords 0..3, so [d, d+1] never wraps
 template <int NB>
@@ -1584,7 +1204,7 @@ __device__ __forceinline__ int bp_generate(const Params &P, WS &w, int lane, con
         bp_to_lds<NB>(P, w, lane, pl);
         WSYNC();
         if (scan_effective_clean<false>(P, w, lane)) break;             // possible_move, :102
-        if (shuffles >= TMG_MAX_SHUFFLES) { fl = FL_ERR; break; }
+        if (shuffles >= kMaxShuffles) { fl = FL_ERR; break; }
         COVER(CV_SHUFFLE_GEN);
         bp_ring_state(J, w, r, g);                                       // shuffle draws from the stream itself
         WSYNC();
@@ -1617,16 +1237,12 @@ __device__ __forceinline__ bool queue_env(SpillQ *q, int lane, int64_t e) {
 
 // lane 0 records st in the sticky status words (a rare path: error / overflow)
 __device__ __forceinline__ void note_status(const Params &P, int lane, uint32_t st) {
-#if TMG_STATUS
     // one word per status bit, each only ever set to 1: plain stores, no atomics
     if (st && lane == 0) {
         if (st & ST_INTERNAL) P.status[0] = 1u;
         if (st & ST_OVERFLOW) P.status[1] = 1u;
         if (st & ST_CALLER) P.status[2] = 1u;
     }
-#else
-    (void)P; (void)lane; (void)st;
-#endif
 }
 
 template <class WS>
@@ -2296,9 +1912,9 @@ __device__ __forceinline__ int board_move(const Params &P, WS &w, int lane, cons
     // <= 128 cells: the per-lane cell coordinates are rebuilt where they are
     // used (a few VALU ops) rather than kept live across the cascade loop,
     // which spilled the 128-cell general kernels to scratch; 512 cells: eight
-    // passes' worth, kept (TMG_CELLS_ONCE)
+    // passes' worth, kept (rebuilding them there measured neutral at c5)
     const auto cells = [&]() {
-        if constexpr (MAXN > 128 && TMG_CELLS_ONCE) return cl;
+        if constexpr (MAXN > 128) return cl;
         else return make_cells<MAXN / 64>(P, loop_lane(lane));
     };
     const int N = P.N;
@@ -2408,8 +2024,6 @@ __device__ __forceinline__ int board_move(const Params &P, WS &w, int lane, cons
         refill(P, w, lane, J, g);
         iters++;
     }
-    STAMP(e, 2);
-    STAMPV(e, 6, iters);
     (void)iters;
     nn = w.sc[SC_NNEW];
     na = w.sc[SC_NACT];
@@ -2418,37 +2032,22 @@ __device__ __forceinline__ int board_move(const Params &P, WS &w, int lane, cons
     if (err || w.sc[SC_ERR]) flags |= FL_ERR;
     // the cascade loop ends only on a line-free board (or an error / overflow)
     flags |= ensure_playable(P, w, lane, J, g, cells(), !ovf && !err && !w.sc[SC_ERR]);   // :381-391
-    STAMP(e, 3);
     return elim;
 }
 
 // ------------------------------------------------------------------ kernels
-template <int MAXN = 128, bool LB = (MAXN > 128)>
 __device__ __forceinline__ LaneJump load_jump(const Params &P, int lane, const Rng &g) {
     const uint64_t *t = P.jump + lane * 4;
     LaneJump J;
     J.Aj = U128{t[0], t[1]};
     J.Gj = U128{t[2], t[3]};
     J.incG = mul128(U128{g.ilo, g.ihi}, J.Gj);
-    J.A64 = J.incG64 = U128{0, 0};
-    if constexpr (MAXN > 128 && LB) {                   // draws of > 128 colours span several batches
-        const uint64_t *u = P.jump + 63 * 4;             // A^64, G_64 (wave-uniform)
-        J.A64 = U128{u[0], u[1]};
-        J.incG64 = mul128(U128{g.ilo, g.ihi}, U128{u[2], u[3]});
-    }
     return J;
 }
 
 __device__ __forceinline__ Rng load_rng(const uint64_t *p) {
     Rng g;
     g.slo = bcast64(p[0]); g.shi = bcast64(p[1]); g.ilo = bcast64(p[2]); g.ihi = bcast64(p[3]); g.h = bcast64(p[4]);
-    return g;
-}
-// the same from a row read one word per lane (lane i holds word i)
-__device__ __forceinline__ Rng rng_from_row(uint64_t row) {
-    Rng g;
-    g.slo = rdlane64(row, 0); g.shi = rdlane64(row, 1); g.ilo = rdlane64(row, 2); g.ihi = rdlane64(row, 3);
-    g.h = rdlane64(row, 4);
     return g;
 }
 __device__ __forceinline__ void store_rng(uint64_t *p, const Rng &g, int lane) {
@@ -2475,24 +2074,18 @@ __device__ __forceinline__ uint32_t step_env(
     // Only the 128-cell lean kernels regenerate a finished board inline
     // (autoreset == 1); do_step (tmg_capi.hip) hands every other kernel
     // autoreset == 2, a masked reset_kernel launch after the step, so they
-    // carry no generate_board code (with TMG_LEAN_DEFER the lean ones neither)
-    constexpr bool INLINE_GEN = !GEN && MAXN == 128 && !TMG_LEAN_DEFER;
-    STAMP(e, 0);
+    // carry no generate_board code
+    constexpr bool INLINE_GEN = !GEN && MAXN == 128;
     const int a = __builtin_amdgcn_readfirstlane(actions[e]);             // wave-uniform loads
     const int t0 = __builtin_amdgcn_readfirstlane(timer[e]);
-    // Issued beside the two loads above, none depending on the action: the
-    // env's cached mask row (lane i holds word i) and its board words.  The
-    // ineffective-move exit then waits for one memory latency instead of the
-    // chain action -> mask word, and the effective path finds its board in
-    // registers.  (The mask row is allocated memory whatever trust_eff says;
-    // it is only read as a mask when trust_eff != 0.)
-    // TMG_PREFETCH: 0 = none (the mask word loaded once the action is known),
-    // 1 = the mask row, 2 = the mask row, board and RNG state
-    const uint64_t effrow = (TMG_PREFETCH >= 1 && lane < W) ? eff[e * W + lane] : 0ULL;
-    const uint64_t rngrow = (TMG_PREFETCH >= 2 && lane < 5) ? rng[e * 5 + lane] : 0ULL;   // lane i: RNG word i
-    BoardPre<MAXN> bpre;
-    if constexpr (TMG_PREFETCH >= 2) board_prefetch(P, bpre, lane, board + e * 2 * N);
-    if constexpr (TMG_PREFETCH >= 1) TMG_KEEP_V(effrow);
+    // Issued beside the two loads above, not depending on the action: the
+    // env's cached mask row (lane i holds word i).  The ineffective-move exit
+    // then waits for one memory latency instead of the chain action -> mask
+    // word.  (The mask row is allocated memory whatever trust_eff says; it is
+    // only read as a mask when trust_eff != 0.)  Loading the board and RNG
+    // state there too measured slower: the quick waves wait for those loads.
+    const uint64_t effrow = lane < W ? eff[e * W + lane] : 0ULL;
+    TMG_KEEP_V(effrow);
     if (t0 >= P.num_moves || a < 0 || a >= P.A) {                           // tile_match_env.py:94-95
         if (lane == 0) { reward[e] = 0; n_new[e] = 0; n_act[e] = 0; flags_out[e] = FL_ERR; }
         if (P.oh && !trust_eff) {             // the fused planes follow every board of an untrusted call
@@ -2509,8 +2102,7 @@ __device__ __forceinline__ uint32_t step_env(
     int flags = done ? FL_DONE : 0;
     bool effective = false;
     if (trust_eff) {                                                        // board.py:352 via cached mask
-        if constexpr (TMG_PREFETCH >= 1) effective = (rdlane64(effrow, a >> 6) >> (a & 63)) & 1ULL;
-        else effective = (bcast64(ge[a >> 6]) >> (a & 63)) & 1ULL;
+        effective = (rdlane64(effrow, a >> 6) >> (a & 63)) & 1ULL;
     }
     if (trust_eff && !effective && !(done && autoreset == 1)) {             // no state change at all
         const bool defer = done && autoreset;                               // autoreset == 2: reset_kernel next
@@ -2519,15 +2111,13 @@ __device__ __forceinline__ uint32_t step_env(
             timer[e] = defer ? 0 : t1; reward[e] = 0; n_new[e] = 0; n_act[e] = 0;
             flags_out[e] = (uint8_t)(flags | (defer ? FL_RESET : 0));
         }
-        STAMP(e, 7);
         return 0;
     }
     int r1, c1, r2, c2;
     action_coords(P.R, P.C, a, r1, c1, r2, c2);
     const int p1 = r1 * P.C + c1, p2 = r2 * P.C + c2;
 
-    if constexpr (TMG_PREFETCH >= 2) board_from_prefetch(P, w, bpre, lane, gb);
-    else load_board(P, w, lane, gb);
+    load_board(P, w, lane, gb);
     if constexpr (GEN) {
         for (int p = lane; p < N; p += 64) w.mark[p] = 0;
     }
@@ -2545,12 +2135,11 @@ __device__ __forceinline__ uint32_t step_env(
         bool ex = lane == 0 ? eff_exact(P, w.brd, a) : false;
         effective = __ballot(ex) != 0ULL;
     }
-    Rng g = TMG_PREFETCH >= 2 ? rng_from_row(rngrow) : load_rng(rng + e * 5);
-    const LaneJump J = load_jump<MAXN, TMG_LANE_BATCH_STEP != 0>(P, lane, g);
+    Rng g = load_rng(rng + e * 5);
+    const LaneJump J = load_jump(P, lane, g);
     const Cells<MAXN / 64> cl = make_cells<MAXN / 64>(P, lane);
     int elim = 0, nn = 0, na = 0;
     bool changed = false;
-    STAMP(e, 1);
     if (effective) {
         if constexpr (SBNB > 0 && !GEN) elim = sb_move<SBNB, CODD>(P, w, lane, J, g, cl, p1, p2, flags, e);
         else elim = board_move<MAXN, GEN, SBNB, CODD, TIER>(P, w, lane, J, g, cl, p1, p2, flags, nn, na, e, lists,
@@ -2571,15 +2160,12 @@ __device__ __forceinline__ uint32_t step_env(
             }
         }
     }
-    STAMP(e, 4);
     int tnew = t1;
     if (done && autoreset) {                                                // reset() without a seed
         if constexpr (INLINE_GEN) {
             if (autoreset == 1) {
                 int fg = -1;
-                if constexpr (SBNB > 0 && !TMG_BP) {
-                    fg = sb_generate<SBNB, CODD, TMG_SB_VDET_STEP != 0>(P, w, lane, J, g, cl);
-                } else if constexpr (SBNB > 0) {
+                if constexpr (SBNB > 0) {
                     if (P.C <= 32) fg = bp_generate<SBNB>(P, w, lane, J, g);
                     if (fg < 0) fg = sb_generate_exact<SBNB, CODD>(P, w, lane, J, g, cl);
                 } else {
@@ -2592,7 +2178,6 @@ __device__ __forceinline__ uint32_t step_env(
         tnew = 0;
         flags |= FL_RESET;
     }
-    STAMP(e, 5);
     if (changed) {
         store_board(P, w, lane, gb);
         store_rng(rng + e * 5, g, lane);
@@ -2616,13 +2201,12 @@ __device__ __forceinline__ uint32_t step_env(
         n_act[e] = na;
         flags_out[e] = (uint8_t)flags;
     }
-    STAMP(e, 7);
     return ((flags & FL_ERR) ? ST_INTERNAL : 0u) | ((flags & FL_OVF) ? ST_OVERFLOW : 0u);
 }
 
 // TileMatchEnv.step over a batch, one wave per env.
 template <int MAXN, bool GEN, int SBNB = 0, bool CODD = false>
-__global__ __launch_bounds__(64 * TMG_WPB, MAXN == 128 ? (GEN ? TMG_GEN128_WAVES : TMG_LEAN128_WAVES) : (GEN ? TMG_GEN512_WAVES : TMG_WPE)) void step_kernel(
+__global__ __launch_bounds__(64, MAXN == 128 ? (GEN ? kGen128Waves : kLean128Waves) : 1) void step_kernel(
     Params P_, int64_t n, int8_t *__restrict__ board, uint64_t *__restrict__ rng, int32_t *__restrict__ timer,
     const int32_t *__restrict__ actions, int32_t *__restrict__ reward, int32_t *__restrict__ n_new,
     int32_t *__restrict__ n_act, uint8_t *__restrict__ flags_out, uint64_t *__restrict__ eff, int trust_eff,
@@ -2631,9 +2215,8 @@ __global__ __launch_bounds__(64 * TMG_WPB, MAXN == 128 ? (GEN ? TMG_GEN128_WAVES
     using WS = Ws<MAXN, GEN>;
     const Params &P = TMG_KERNARG_PARAMS(P_);
     const int lane = threadIdx.x & 63;
-    const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
-    WS &w = reinterpret_cast<WS *>(smem)[wv];
-    const int64_t e = wg_env0() + wv;
+    WS &w = *reinterpret_cast<WS *>(smem);
+    const int64_t e = wg_env();
     if (e >= n) return;
     WsSerial<MAXN> *lists = nullptr;
     if constexpr (GEN) lists = &w.s;
@@ -2645,19 +2228,16 @@ __global__ __launch_bounds__(64 * TMG_WPB, MAXN == 128 ? (GEN ? TMG_GEN128_WAVES
 // Re-runs the steps the general step kernel queued on running out of LDS list
 // space (step_env, FL_OVF), on global-memory lists sized for the worst case
 // (WsSerialBig): launched right after every general step launch on the same
-// stream with the same buffers, TMG_SPILL_WAVES one-wave workgroups, each
+// stream with the same buffers, kSpillWaves one-wave workgroups, each
 // with its own WsSerialBig.  An empty queue costs one load per wave.  The
 // generic (non-bitboard) path: bit-identical results by construction.
-// Small footprint on purpose (no LDS lists, at most TMG_SPILL_VGPR_WAVES'
-// worth of VGPRs, spilling to scratch instead): the launch follows every
+// Small footprint on purpose (no LDS lists, at most 8 waves/SIMD's worth of
+// VGPRs, spilling to scratch instead): the launch follows every
 // general step on its stream and must find room on a chip busy with the
 // other streams' kernels at once, or it holds its stream back; the rare
 // steps it re-runs may go slowly.
-#ifndef TMG_SPILL_VGPR_WAVES
-#define TMG_SPILL_VGPR_WAVES 8
-#endif
 template <int MAXN>
-__global__ __launch_bounds__(64, TMG_SPILL_VGPR_WAVES) void spill_kernel(
+__global__ __launch_bounds__(64, 8) void spill_kernel(
     Params P, int64_t n, int8_t *__restrict__ board, uint64_t *__restrict__ rng, int32_t *__restrict__ timer,
     const int32_t *__restrict__ actions, int32_t *__restrict__ reward, int32_t *__restrict__ n_new,
     int32_t *__restrict__ n_act, uint8_t *__restrict__ flags_out, uint64_t *__restrict__ eff, int trust_eff,
@@ -2694,23 +2274,17 @@ __device__ __forceinline__ void reset_env(const Params &P, WS &w, int lane, int6
                                           uint64_t *__restrict__ eff) {
     const int N = P.N, W = P.W;
     Rng g = load_rng(rng + e * 5);
-    const LaneJump J = load_jump<MAXN, TMG_LANE_BATCH != 0>(P, lane, g);
+    const LaneJump J = load_jump(P, lane, g);
     const Cells<MAXN / 64> cl = make_cells<MAXN / 64>(P, lane);
     // board.py:95-109: on row bit-planes (C <= 32); a Lemire rejection or a
     // wider board takes the exact draw-by-draw path
     int fl = -1;
-    if constexpr (SBNB > 0 && TMG_BP) {
+    if constexpr (SBNB > 0) {
         if (P.C <= 32) fl = bp_generate<SBNB>(P, w, lane, J, g);
     }
     if (fl < 0) {
-        if constexpr (MAXN == 128 && SBNB > 0) {
-            if constexpr (TMG_BP) fl = sb_generate_exact<SBNB, CODD>(P, w, lane, J, g, cl);
-            else fl = sb_generate<SBNB, CODD, TMG_SB_VDET != 0>(P, w, lane, J, g, cl);
-        } else if constexpr (MAXN > 128 && !TMG_BP) {
-            fl = generate_board_ring(P, w, lane, J, g, cl);
-        } else {
-            fl = generate_board(P, w, lane, J, g, cl);
-        }
+        if constexpr (MAXN == 128 && SBNB > 0) fl = sb_generate_exact<SBNB, CODD>(P, w, lane, J, g, cl);
+        else fl = generate_board(P, w, lane, J, g, cl);
     }
     note_status(P, lane, fl ? ST_INTERNAL : 0u);
     store_board(P, w, lane, board + e * 2 * N);
@@ -2721,7 +2295,7 @@ __device__ __forceinline__ void reset_env(const Params &P, WS &w, int lane, int6
 }
 
 template <int MAXN, int SBNB = 0, bool CODD = false>
-__global__ __launch_bounds__(64 * TMG_WPB, MAXN > 128 ? TMG_RESET512_WAVES : 1) void reset_kernel(Params P_, int64_t n, int8_t *__restrict__ board,
+__global__ __launch_bounds__(64, MAXN > 128 ? kReset512Waves : 1) void reset_kernel(Params P_, int64_t n, int8_t *__restrict__ board,
                                                              uint64_t *__restrict__ rng, int32_t *__restrict__ timer,
                                                              uint64_t *__restrict__ eff,
                                                              const uint8_t *__restrict__ env_mask, int mask_bits) {
@@ -2729,9 +2303,8 @@ __global__ __launch_bounds__(64 * TMG_WPB, MAXN > 128 ? TMG_RESET512_WAVES : 1) 
     using WS = Ws<MAXN, false>;
     const Params &P = TMG_KERNARG_PARAMS(P_);
     const int lane = threadIdx.x & 63;
-    const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
-    WS &w = reinterpret_cast<WS *>(smem)[wv];
-    const int64_t e = wg_env0() + wv;
+    WS &w = *reinterpret_cast<WS *>(smem);
+    const int64_t e = wg_env();
     if (e >= n) return;
     if (env_mask && !(__builtin_amdgcn_readfirstlane((int)env_mask[e]) & mask_bits)) return;
     reset_env<MAXN, SBNB, CODD>(P, w, lane, e, board, rng, timer, eff);
@@ -2739,14 +2312,13 @@ __global__ __launch_bounds__(64 * TMG_WPB, MAXN > 128 ? TMG_RESET512_WAVES : 1) 
 
 // TileMatchEnv._get_effective_actions for arbitrary boards (tile_match_env.py:118-124)
 template <int MAXN>
-__global__ TMG_LAUNCH_BOUNDS void effective_kernel(Params P, int64_t n, const int8_t *__restrict__ board,
+__global__ __launch_bounds__(64) void effective_kernel(Params P, int64_t n, const int8_t *__restrict__ board,
                                                                  uint64_t *__restrict__ eff) {
     TMG_SMEM_DECL(smem);
     using WS = Ws<MAXN, false>;
     const int lane = threadIdx.x & 63;
-    const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
-    WS &w = reinterpret_cast<WS *>(smem)[wv];
-    const int64_t e = wg_env0() + wv;
+    WS &w = *reinterpret_cast<WS *>(smem);
+    const int64_t e = wg_env();
     if (e >= n) return;
     load_board(P, w, lane, board + e * 2 * P.N);
     WSYNC();

@@ -45,7 +45,6 @@ struct tmg_ctx {
     uint64_t *d_sbrows;
     uint32_t *d_status;  // sticky status words (tmg_status): one per TMG_STATUS_* bit
     unsigned long long *d_cover;   // TMG_COVER builds only
-    uint64_t *d_stamps;            // TMG_STAMPS builds only
     int maxn;
     int sb;              // scalar-bitboard kernels (<= 128 cells, C <= 63)
     int scan_only;       // tmg_create_scan: tmg_effective / tmg_onehot only
@@ -67,9 +66,7 @@ using tmg::StepArgs;
 
 namespace tmg {
 dim3 env_grid(int64_t n) {
-    int64_t nwg = (n + TMG_WPB - 1) / TMG_WPB;
-    if (TMG_XCD) nwg = (nwg + 7) & ~(int64_t)7;
-    return dim3((unsigned)nwg);
+    return dim3((unsigned)((n + 7) & ~(int64_t)7));   // one wave per env, 8 equal XCD blocks (wg_env)
 }
 size_t spill_ws_bytes(int maxn) {
     return maxn <= 128 ? sizeof(WsSerialBig<128>) : sizeof(WsSerialBig<512>);
@@ -102,7 +99,7 @@ static int spill_for(tmg_ctx *ctx, hipStream_t s, int64_t n, tmg::SpillQ **q, vo
     if (!sp) {
         ctx->spills.push_back(tmg_ctx::Spill{s, nullptr, 0, nullptr});
         sp = &ctx->spills.back();
-        int rc = hip_check(hipMalloc(&sp->ws, tmg::spill_ws_bytes(ctx->maxn) * TMG_SPILL_WAVES), "hipMalloc");
+        int rc = hip_check(hipMalloc(&sp->ws, tmg::spill_ws_bytes(ctx->maxn) * tmg::kSpillWaves), "hipMalloc");
         if (rc) { ctx->spills.pop_back(); return rc; }
     }
     if (sp->cap < n) {
@@ -148,7 +145,7 @@ static int do_step(tmg_ctx *ctx, Params P, StepArgs a, hipStream_t s) {
     a.autoreset = a.autoreset ? 1 : 0;
     // the general and 512-cell kernels leave finished boards to a reset launch
     // masked by FL_RESET, which runs at several times their occupancy
-    const int deferred = a.autoreset && (ctx->maxn == 512 || !lean || TMG_LEAN_DEFER);
+    const int deferred = a.autoreset && (ctx->maxn == 512 || !lean);
     if (!lean) {
         int rc = spill_for(ctx, s, a.n, &P.spill, &P.spill_ws);
         if (rc) return rc;
@@ -297,16 +294,11 @@ int alloc_tables(tmg_ctx *c) {
     if (!rc) rc = hip_check(hipMalloc(&c->d_cover, tmg::CV_COUNT * sizeof(unsigned long long)), "hipMalloc");
     if (!rc) rc = hip_check(hipMemset(c->d_cover, 0, tmg::CV_COUNT * sizeof(unsigned long long)), "hipMemset");
 #endif
-#if TMG_STAMPS
-    if (!rc) rc = hip_check(hipMalloc(&c->d_stamps, (size_t)tmg::kStampEnvs * tmg::kStampSlots * 8), "hipMalloc");
-    if (!rc) rc = hip_check(hipMemset(c->d_stamps, 0, (size_t)tmg::kStampEnvs * tmg::kStampSlots * 8), "hipMemset");
-#endif
     if (!rc) rc = hip_check(hipDeviceSynchronize(), "hipDeviceSynchronize");
     P.jump = c->d_jump;
     P.status = c->d_status;
     P.sb_rows = c->d_sbrows;
     P.cover = c->d_cover;
-    P.stamps = c->d_stamps;
     return rc;
 }
 
@@ -315,7 +307,6 @@ void free_ctx(tmg_ctx *c) {
     if (c->d_status) (void)hipFree(c->d_status);
     if (c->d_sbrows) (void)hipFree(c->d_sbrows);
     if (c->d_cover) (void)hipFree(c->d_cover);
-    if (c->d_stamps) (void)hipFree(c->d_stamps);
     for (const auto &x : c->spills) {
         if (x.q) (void)hipFree(x.q);
         if (x.ws) (void)hipFree(x.ws);
@@ -332,7 +323,7 @@ int new_ctx(tmg_ctx **out, int device, int rows, int cols, int colours, uint32_t
     if (rc) return rc;
     tmg_ctx *c = new tmg_ctx();
     c->device = device;
-    c->d_jump = nullptr; c->d_sbrows = nullptr; c->d_status = nullptr; c->d_cover = nullptr; c->d_stamps = nullptr;
+    c->d_jump = nullptr; c->d_sbrows = nullptr; c->d_status = nullptr; c->d_cover = nullptr;
     c->P = tmg::make_params(rows, cols, colours, (int)specials_mask, num_moves, nullptr);
     c->maxn = c->P.N <= 128 ? 128 : 512;
     c->sb = c->P.N <= 128 && c->P.C <= 63;
@@ -553,18 +544,6 @@ int tmg_count_states(int device, int rows, int cols, int colours, uint64_t *num_
     *num_line_free = h[1];
     return 0;
 }
-
-#if TMG_STAMPS
-// diagnostic build only: copy the per-env phase stamps (uint64 [n][8]) to host memory
-__attribute__((visibility("default"))) int tmg_debug_stamps(tmg_ctx *ctx, uint64_t *host, int64_t n) {
-    if (!ctx || !ctx->d_stamps) return fail(-1, "no stamps");
-    if (n > tmg::kStampEnvs) n = tmg::kStampEnvs;
-    int rc = hip_check(hipDeviceSynchronize(), "hipDeviceSynchronize");
-    if (!rc) rc = hip_check(hipMemcpy(host, ctx->d_stamps, (size_t)n * tmg::kStampSlots * 8, hipMemcpyDeviceToHost),
-                            "hipMemcpy");
-    return rc;
-}
-#endif
 
 #if TMG_COVER
 // diagnostic build only: the CV_* branch hit counters of this context

@@ -20,8 +20,8 @@ namespace {
 
 template <int MAXN, bool GEN, int NB, bool CODD>
 void step_one(dim3 grid, hipStream_t s, const Params &P, const StepArgs &a) {
-    const size_t lds = sizeof(Ws<MAXN, GEN>) * TMG_WPB;
-    hipLaunchKernelGGL((step_kernel<MAXN, GEN, NB, CODD>), grid, dim3(64 * TMG_WPB), lds, s, P, a.n, a.board, a.rng,
+    const size_t lds = sizeof(Ws<MAXN, GEN>);
+    hipLaunchKernelGGL((step_kernel<MAXN, GEN, NB, CODD>), grid, dim3(64), lds, s, P, a.n, a.board, a.rng,
                        a.timer, a.actions, a.reward, a.n_new, a.n_act, a.flags, a.eff, a.trust_eff, a.autoreset);
 }
 
@@ -39,21 +39,21 @@ void step_sb(dim3 grid, hipStream_t s, const Params &P, const StepArgs &a) {
 template <int MAXN>
 void spill_one(hipStream_t s, const Params &P, const StepArgs &a) {
     const size_t lds = sizeof(Ws<MAXN, false>);
-    hipLaunchKernelGGL((spill_kernel<MAXN>), dim3(TMG_SPILL_WAVES), dim3(64), lds, s, P, a.n, a.board, a.rng, a.timer,
+    hipLaunchKernelGGL((spill_kernel<MAXN>), dim3(kSpillWaves), dim3(64), lds, s, P, a.n, a.board, a.rng, a.timer,
                        a.actions, a.reward, a.n_new, a.n_act, a.flags, a.eff, a.trust_eff, a.autoreset);
 }
 
 template <int MAXN, int NB, bool CODD>
 void reset_one(dim3 grid, hipStream_t s, const Params &P, int64_t n, int8_t *board, uint64_t *rng, int32_t *timer,
                uint64_t *eff, const uint8_t *env_mask, int mask_bits) {
-    const size_t lds = sizeof(Ws<MAXN, false>) * TMG_WPB;
-    hipLaunchKernelGGL((reset_kernel<MAXN, NB, CODD>), grid, dim3(64 * TMG_WPB), lds, s, P, n, board, rng, timer, eff,
+    const size_t lds = sizeof(Ws<MAXN, false>);
+    hipLaunchKernelGGL((reset_kernel<MAXN, NB, CODD>), grid, dim3(64), lds, s, P, n, board, rng, timer, eff,
                        env_mask, mask_bits);
 }
 
 template <int MAXN>
 void effective_one(dim3 grid, hipStream_t s, const Params &P, int64_t n, const int8_t *board, uint64_t *eff) {
-    hipLaunchKernelGGL(effective_kernel<MAXN>, grid, dim3(64 * TMG_WPB), sizeof(Ws<MAXN, false>) * TMG_WPB, s, P, n,
+    hipLaunchKernelGGL(effective_kernel<MAXN>, grid, dim3(64), sizeof(Ws<MAXN, false>), s, P, n,
                        board, eff);
 }
 

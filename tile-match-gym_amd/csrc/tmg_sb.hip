@@ -12,15 +12,6 @@
 // gravity/refill scatter.  The int8 LDS board stays in sync at the points the
 // shared code reads it (effective-action scan, shuffle, store).
 
-#ifndef TMG_SB_VDET
-#define TMG_SB_VDET 1        // reset kernel: remove_colour_lines' line search on the lane codes (VALU)
-#endif
-#ifndef TMG_SB_RING
-#define TMG_SB_RING 1        // generate_board's colours through the LDS colour ring (sb_generate)
-#endif
-#ifndef TMG_SB_VDET_STEP
-#define TMG_SB_VDET_STEP 1   // the same in the step kernels' inline autoreset (c2: 6.77 -> 7.24 x 10^8)
-#endif
 
 struct Pair {
     uint64_t a, b;
@@ -171,60 +162,6 @@ __device__ __forceinline__ void sb_line_keys(const Params &P, int lane, int &key
     const int r0 = div_c(P, q0), r1 = div_c(P, q1);
     keyA = q0 < P.N ? ((r0 << 8) | (255 - (q0 - r0 * P.C))) << 1 : -1;
     keyB = q1 < P.N ? ((r1 << 8) | (255 - (q1 - r1 * P.C))) << 1 : -1;
-}
-
-// remove_colour_lines' line search with the anchors evaluated on the lane
-// codes themselves (VALU), no bitboards: lane j holds cells 2j (a) and 2j+1
-// (b); the cell to the right of b is lane j+1's a (DPP wave_shl:1), the cells
-// one and two rows up sit C/2 and C lanes lower for even C (same half), and
-// for odd C one row up swaps halves ((C+1)/2 or (C-1)/2 lanes lower).  The
-// anchor conditions are get_colour_lines' (board.py:163-193, every type 1
-// here); the key is sb_first_line_key's.  Valid-anchor masks exclude cells
-// whose neighbours would fall off the board, so wrapped lanes never count.
-struct SBVKey {
-    int key;                 // max key over anchors, -1: no line
-    uint64_t eqa, eqb;       // ballots: cell a / b has the colour of the cell above (vertical walk)
-};
-__device__ __forceinline__ int lane_up(int v, int lane, int d) {            // value of lane - d
-    return __builtin_amdgcn_ds_bpermute((lane - d) << 2, v);
-}
-template <bool CODD>
-__device__ __forceinline__ SBVKey sb_first_line_key_v(const Params &P, const SBC &c, int lane, int keyA, int keyB,
-                                                      int vokA, int vokB, int hokA, int hokB) {
-    const int C = P.C;
-    const int pk = c.a | (c.b << 8);
-    const int nx = __builtin_amdgcn_update_dpp(0, pk, 0x130, 0xf, 0xf, false);   // wave_shl:1: lane j+1
-    const int na = nx & 0xff, nb = nx >> 8;
-    int ua1, ub1, ua2, ub2;                                  // codes one / two rows above a and b
-    if constexpr (CODD) {
-        ua1 = lane_up(pk, lane, (C + 1) >> 1) >> 8;
-        ub1 = lane_up(pk, lane, (C - 1) >> 1) & 0xff;
-        const int u2 = lane_up(pk, lane, C);
-        ua2 = u2 & 0xff;
-        ub2 = u2 >> 8;
-    } else {
-        const int u1 = lane_up(pk, lane, C >> 1), u2 = lane_up(pk, lane, C);
-        ua1 = u1 & 0xff; ub1 = u1 >> 8;
-        ua2 = u2 & 0xff; ub2 = u2 >> 8;
-    }
-    const bool eA = c.a == ua1, eB = c.b == ub1;
-    const int vA = vokA & (eA & (c.a == ua2)), vB = vokB & (eB & (c.b == ub2));
-    const int hA = hokA & ((c.a == c.b) & (c.a == na)), hB = hokB & ((c.b == na) & (c.b == nb));
-    const int ka = (vA | hA) ? keyA | vA : -1, kb = (vB | hB) ? keyB | vB : -1;
-    SBVKey r;
-    r.key = wave_max(ka > kb ? ka : kb);
-    r.eqa = __ballot(eA);
-    r.eqb = __ballot(eB);
-    return r;
-}
-// the row of the first coord of that line (vertical: the top of its run)
-__device__ __forceinline__ int sb_line_row_of_key_v(const Params &P, const SBVKey &k) {   // k.key >= 0
-    const int rs = k.key >> 9;
-    if (!(k.key & 1)) return rs;
-    const int C = P.C;
-    int t = (rs - 2) * C + 255 - ((k.key >> 1) & 255);
-    while (t >= C && ((((t & 1) ? k.eqb : k.eqa) >> (t >> 1)) & 1ULL)) t -= C;
-    return div_c(P, t);
 }
 
 // The first-pass coords of get_colour_lines' bottom row rs (board.py:158-193):
@@ -443,38 +380,22 @@ __device__ __forceinline__ void sb_draw_rows(const Params &P, WS &w, int lane, c
 // scan (whose mask it leaves in w.effw) and the shuffle.  `dirty`: c is newer
 // than the LDS board; `clean`: the board is known to hold no line.  Returns
 // FL_SHUF when a shuffle ran, FL_ERR when the shuffle cap ended the loop.
-// VDET: the line search on the lane codes (sb_first_line_key_v) instead of
-// the bitboards.  Used by reset_kernel only: in the lean step kernel it costs
-// registers on the normal-step path (A/B).
-template <int NB, bool CODD, bool VDET = false, bool GEN = false, class WS>
+// GEN: the loop of generate_board (the cover counters tell the two apart).
+template <int NB, bool CODD, bool GEN = false, class WS>
 __device__ __forceinline__ int sb_ensure(const Params &P, WS &w, int lane, const LaneJump &J, Rng &g,
                                          const Cells<WS::NP> &cl, SBC &c, bool dirty, bool clean) {
     int keyA, keyB;
     sb_line_keys(P, lane, keyA, keyB);
-    int vokA = 0, vokB = 0, hokA = 0, hokB = 0;
-    if constexpr (VDET) {
-        vokA = (int)(P.sb_v[0] >> lane) & 1; vokB = (int)(P.sb_v[1] >> lane) & 1;
-        hokA = (int)(P.sb_h[0] >> lane) & 1; hokB = (int)(P.sb_h[1] >> lane) & 1;
-    }
     int fl = 0;
     for (int shuffles = 0;; shuffles++) {
         if (!clean) {
             for (;;) {
                 const SBDrawPre pre = sb_draw_pre(J, g);
-                int key, r0 = 0;
-                if constexpr (VDET) {
-                    const SBVKey kv = sb_first_line_key_v<CODD>(P, c, lane, keyA, keyB, vokA, vokB, hokA, hokB);
-                    key = kv.key;
-                    TMG_KEEP_V3(pre.sj.lo, pre.sj.hi, pre.out);   // keep the jump-ahead above the exit test
-                    if (key < 0) break;
-                    r0 = sb_line_row_of_key_v(P, kv);
-                } else {
-                    const SBDet d = sb_detect<NB, CODD>(P, sb_planes_of<NB>(c));
-                    key = sb_first_line_key<NB, CODD>(P, d, lane, keyA, keyB);
-                    TMG_KEEP_V3(pre.sj.lo, pre.sj.hi, pre.out);   // keep the jump-ahead above the exit test
-                    if (key < 0) break;
-                    r0 = sb_line_row_of_key<CODD>(P, d, key);
-                }
+                const SBDet d = sb_detect<NB, CODD>(P, sb_planes_of<NB>(c));
+                const int key = sb_first_line_key<NB, CODD>(P, d, lane, keyA, keyB);
+                TMG_KEEP_V3(pre.sj.lo, pre.sj.hi, pre.out);   // keep the jump-ahead above the exit test
+                if (key < 0) break;
+                const int r0 = sb_line_row_of_key<CODD>(P, d, key);
                 const int row = P.R - 1 < r0 + 1 ? P.R - 1 : r0 + 1;   // colour plane only, rows 0..row
                 sb_draw_rows<NB>(P, w, lane, J, g, row, c, pre);
                 dirty = true;
@@ -487,7 +408,7 @@ __device__ __forceinline__ int sb_ensure(const Params &P, WS &w, int lane, const
             dirty = false;
         }
         if (scan_effective_clean<false>(P, w, lane)) break;   // types all 1, no line
-        if (shuffles >= TMG_MAX_SHUFFLES) { fl |= FL_ERR; break; }
+        if (shuffles >= kMaxShuffles) { fl |= FL_ERR; break; }
         COVER(GEN ? CV_SHUFFLE_GEN : CV_SHUFFLE);
         WSYNC();
         shuffle(P, w, lane, g);
@@ -499,97 +420,17 @@ __device__ __forceinline__ int sb_ensure(const Params &P, WS &w, int lane, const
     return fl;
 }
 
-// generate_board, board.py:95-109 (types all 1; colours from the env stream);
-// returns FL_ERR when a safety cap was hit
-template <int NB, bool CODD, bool VDET = false, class WS>
+// generate_board, board.py:95-109 (types all 1; colours from the env stream),
+// draw by draw on the scalar bitboards: boards of C > 32 columns and the exact
+// redo after a Lemire rejection (bp_generate otherwise); returns FL_ERR when
+// a safety cap was hit
+template <int NB, bool CODD, class WS>
 __device__ __forceinline__ int sb_generate_exact(const Params &P, WS &w, int lane, const LaneJump &J, Rng &g,
                                                  const Cells<WS::NP> &cl) {
     SBC c{0, 0};
     sb_draw_rows<NB>(P, w, lane, J, g, P.R - 1, c, sb_draw_pre(J, g));
     for (int p = lane; p < P.N; p += 64) w.brd[P.N + p] = 1;
-    return sb_ensure<NB, CODD, VDET, true>(P, w, lane, J, g, cl, c, true, false) & FL_ERR;
-}
-
-// rows 0..M/C-1 of the lane codes <- the ring's next M colours (ring_take for
-// the lane-side board: lane j holds cells 2j and 2j+1)
-template <class WS>
-__device__ __forceinline__ void sb_ring_take(const Params &P, WS &w, int lane, const LaneJump &J, ColourRing &r, int M,
-                                             SBC &c) {
-    while (r.fill - r.cons < M) ring_fill(P, w, lane, J, r);
-    WSYNC();
-    const uint8_t *ring = ring_bytes(w);
-    const int q0 = 2 * lane;
-    const int x0 = ring[(r.cons + q0) & (kRing - 1)], x1 = ring[(r.cons + q0 + 1) & (kRing - 1)];
-    c.a = q0 < M ? x0 - 1 : c.a;
-    c.b = q0 + 1 < M ? x1 - 1 : c.b;
-    r.cons += M;
-}
-
-// generate_board (board.py:95-109) for the scalar-bitboard kernels with the
-// redraws' colours taken from the LDS colour ring (tmg_board.hip): a 10x10
-// redraw uses ~33 PCG64 outputs, where drawing it on its own costs a whole
-// 64-output jump-ahead batch.  The line search is sb_ensure's (lane codes,
-// VDET; bitboards otherwise).  A Lemire rejection redoes the board with
-// sb_generate_exact from the starting state.
-template <int NB, bool CODD, bool VDET = false, class WS>
-__device__ __forceinline__ int sb_generate(const Params &P, WS &w, int lane, const LaneJump &J, Rng &g,
-                                           const Cells<WS::NP> &cl) {
-    if constexpr (!TMG_SB_RING) return sb_generate_exact<NB, CODD, VDET>(P, w, lane, J, g, cl);
-    const Rng g0 = g;
-    int keyA, keyB;
-    sb_line_keys(P, lane, keyA, keyB);
-    int vokA = 0, vokB = 0, hokA = 0, hokB = 0;
-    if constexpr (VDET) {
-        vokA = (int)(P.sb_v[0] >> lane) & 1; vokB = (int)(P.sb_v[1] >> lane) & 1;
-        hokA = (int)(P.sb_h[0] >> lane) & 1; hokB = (int)(P.sb_h[1] >> lane) & 1;
-    }
-    ColourRing r;
-    ring_init(P, w, lane, g, r);
-    SBC c{0, 0};
-    sb_ring_take(P, w, lane, J, r, P.N, c);
-    for (int p = lane; p < P.N; p += 64) w.brd[P.N + p] = 1;
-    int fl = 0;
-    for (int shuffles = 0;; shuffles++) {
-        for (;;) {
-            if (r.fill - r.cons < 128) ring_fill(P, w, lane, J, r);   // the next redraw's batch, beside the search
-            int key, r0 = 0;
-            if constexpr (VDET) {
-                const SBVKey kv = sb_first_line_key_v<CODD>(P, c, lane, keyA, keyB, vokA, vokB, hokA, hokB);
-                key = kv.key;
-                if (key < 0) break;
-                r0 = sb_line_row_of_key_v(P, kv);
-            } else {
-                const SBDet d = sb_detect<NB, CODD>(P, sb_planes_of<NB>(c));
-                key = sb_first_line_key<NB, CODD>(P, d, lane, keyA, keyB);
-                if (key < 0) break;
-                r0 = sb_line_row_of_key<CODD>(P, d, key);
-            }
-            const int row = P.R - 1 < r0 + 1 ? P.R - 1 : r0 + 1;      // remove_colour_lines: rows 0..row
-            sb_ring_take(P, w, lane, J, r, (row + 1) * P.C, c);
-        }
-        if (r.rej) break;
-        WFENCE();
-        sb_codes_to_lds(P, w.brd, w.trash, lane, c);
-        WSYNC();
-        if (scan_effective_clean<false>(P, w, lane)) break;          // types all 1, no line
-        if (shuffles >= TMG_MAX_SHUFFLES) { fl = FL_ERR; break; }
-        COVER(CV_SHUFFLE);
-        ring_state(J, r, g);                                         // shuffle draws from the stream itself
-        WSYNC();
-        shuffle(P, w, lane, g);
-        c = sb_codes_from_lds(P, w.brd, lane);
-        fl = FL_SHUF;
-        ring_init(P, w, lane, g, r);
-    }
-    if (r.rej) {                                                     // redo draw by draw (P(reject) = thr / 2^32)
-        COVER(CV_REJECT);
-        g = g0;
-        WSYNC();
-        return sb_generate_exact<NB, CODD, VDET>(P, w, lane, J, g, cl);
-    }
-    ring_state(J, r, g);
-    WSYNC();
-    return fl & FL_ERR;
+    return sb_ensure<NB, CODD, true>(P, w, lane, J, g, cl, c, true, false) & FL_ERR;
 }
 
 // Board.move, board.py:330-395, for a board that can hold no special (every
@@ -617,9 +458,7 @@ __device__ __forceinline__ int sb_move(const Params &P, WS &w, int lane, const L
         elim += tot;                                     // R*C - nnz(type) after the resolve (:374)
         sb_gravity_refill<CODD>(P, w, lane, J, g, clr, tot, c);
     }
-    STAMP(e, 2);
     flags |= sb_ensure<NB, CODD>(P, w, lane, J, g, cl, c, false, true);   // :381-391
-    STAMP(e, 3);
     return elim;
 }
 

@@ -197,7 +197,7 @@ static void run_grid(int64_t nblocks, size_t lds, F kernel) {
 template <class F>
 static void run_blocks(int64_t n, size_t lds, F kernel) {
     int64_t nblocks = n;
-    if (TMG_XCD) nblocks = (nblocks + 7) & ~(int64_t)7;
+    nblocks = (nblocks + 7) & ~(int64_t)7;
     run_grid(nblocks, lds, kernel);
 }
 
@@ -206,7 +206,7 @@ static uint32_t g_status[4];
 static std::vector<int64_t> g_spill_buf;          // a SpillQ with room for every env of the call
 static unsigned long long g_spill_total = 0;
 static unsigned long long g_cover[tmg::CV_COUNT];
-static std::vector<unsigned char> g_spill_ws(sizeof(tmg::WsSerialBig<512>) * TMG_SPILL_WAVES);
+static std::vector<unsigned char> g_spill_ws(sizeof(tmg::WsSerialBig<512>) * tmg::kSpillWaves);
 static tmg::SpillQ *spill_queue(std::vector<int64_t> &buf, int64_t n) {
     const size_t words = (sizeof(tmg::SpillQ) + (size_t)n * 8 + 7) / 8;
     buf.assign(words, 0);
@@ -252,7 +252,7 @@ static void emu_step_kernel(EmuStep &S) {
 template <int MAXN>
 static void emu_spill(EmuStep &S) {
     const tmg::Params &P = *S.P;
-    run_grid(TMG_SPILL_WAVES, sizeof(tmg::Ws<MAXN, false>), [&] { tmg::spill_kernel<MAXN>(P, S.n, S.board, S.rng, S.timer, S.actions, S.reward, S.n_new, S.n_act, S.flags, S.eff, S.trust_eff, S.autoreset); });
+    run_grid(tmg::kSpillWaves, sizeof(tmg::Ws<MAXN, false>), [&] { tmg::spill_kernel<MAXN>(P, S.n, S.board, S.rng, S.timer, S.actions, S.reward, S.n_new, S.n_act, S.flags, S.eff, S.trust_eff, S.autoreset); });
 }
 
 template <bool GEN, bool CODD>
@@ -314,7 +314,7 @@ int emu_step(int R, int C, int k, int smask, int moves, int64_t n, int8_t *board
     S.autoreset = autoreset ? 1 : 0;
     // as tmg_capi.hip's do_step: the general and 512-cell kernels leave
     // finished boards to a reset launch masked by FL_RESET
-    const int deferred = S.autoreset && (P.N > 128 || !lean || TMG_LEAN_DEFER);
+    const int deferred = S.autoreset && (P.N > 128 || !lean);
     if (deferred) S.autoreset = 2;
     if (P.N <= 128) {
         if (lean) {
