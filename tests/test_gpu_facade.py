@@ -85,3 +85,29 @@ def test_is_move_effective_any_shape():
             assert np.array_equal(got, want), (R, C, b)
             bd = Board(R, C, 3, [], [], board=b)
             assert bd.possible_move() == any_ and bd.possible_move(b) == any_
+
+
+@pytest.mark.gpu
+def test_possible_move_other_shape_grid():
+    """Board.possible_move(grid) with a grid of another shape: the reference
+    loops over the Board's OWN action table (board.py:564-568), so the answer
+    is whether one of those coordinate pairs is effective on the grid (larger
+    grids), and a grid too small for the first non-effective coordinates
+    raises IndexError (numpy indexing)."""
+    from oracle import oracle as orc
+    from tile_match_gym_amd.tile_match_env import Board, action_to_coords
+    rs = np.random.default_rng(31)
+    bd = Board(4, 4, 3, [], [], board=np.ones((4, 4), np.int32))
+    checked = 0
+    for R, C in ((5, 6), (6, 4), (4, 7), (8, 8)):
+        for _ in range(40):
+            g = np.stack([rs.integers(1, 4, (R, C)), np.ones((R, C), np.int64)]).astype(np.int32)
+            mask, _ = orc.effective_mask(g.astype(np.int8))
+            own = {pair: i for i, pair in enumerate(action_to_coords(R, C))}
+            want = any(mask[own[pair]] for pair in action_to_coords(4, 4))
+            assert bd.possible_move(g) == want, (R, C)
+            checked += 1
+    small = np.stack([np.array([[1, 2, 3], [2, 3, 1], [3, 1, 2]]), np.ones((3, 3), np.int64)]).astype(np.int32)
+    with pytest.raises(IndexError):
+        bd.possible_move(small)                  # no effective move before (3, 0)-(3, 1) falls off the grid
+    assert checked == 160

@@ -47,7 +47,7 @@ struct tmg_ctx {
     unsigned long long *d_cover;   // TMG_COVER builds only
     int maxn;
     int sb;              // scalar-bitboard kernels (<= 128 cells, C <= 63)
-    int scan_only;       // tmg_create_scan: tmg_effective / tmg_onehot only
+    int scan_only;       // tmg_create_scan: tmg_effective only
     // spill queue of the general kernels, one per stream the context steps on
     // (a queue is only ever touched by the launches of its own stream, in
     // order), holding at least as many entries as the largest launch on it
@@ -178,7 +178,7 @@ static int check_call(tmg_ctx *ctx, int64_t n) {
 
 static int check_full(tmg_ctx *ctx, int64_t n) {
     int rc = check_call(ctx, n);
-    if (!rc && ctx->scan_only) return fail(-2, "context made by tmg_create_scan: effective / onehot only");
+    if (!rc && ctx->scan_only) return fail(-2, "context made by tmg_create_scan: tmg_effective only");
     return rc;
 }
 
@@ -242,16 +242,17 @@ bool shape_viable(int R, int C, int k) {
     const int kk = k < 16 ? k : 16;
     std::vector<int> order(N * 16), next(N, 0);       // per cell: a random colour order, the next one to try
     long budget = 1L << 22;                            // cell assignments over the whole search
-    int complete = 0;
     for (int restart = 0; restart < 64 && budget > 0; restart++) {
-        int p = 0;
+        int p = 0, complete = 0;
         next[0] = 0;
         for (int v = 0; v < kk; v++) order[v] = v;
         for (int v = kk - 1; v > 0; v--) std::swap(order[v], order[rnd() % (v + 1)]);
         while (p >= 0 && budget-- > 0) {
             if (p == N) {
                 if (playable(b.data(), R, C)) return true;
-                if (++complete > 4096) return false;   // many line-free boards, none playable
+                // backtracking only varies the last cells: after many line-free
+                // boards with no playable swap, try another random order
+                if (++complete > 4096) break;
                 p--;
                 continue;
             }

@@ -178,7 +178,27 @@ class Board:
         return _effective_actions(self.board, self._device)
 
     def possible_move(self, grid=None) -> bool:                              # board.py:558-569
-        return bool(_effective_actions(self.board if grid is None else np.asarray(grid), self._device))
+        """Whether any of THIS board's actions (self.action_to_coords, in index
+        order) is effective on `grid` (default: self.board), as the reference
+        loops over its own action table whatever grid is passed: a grid of
+        another shape is checked at those coordinates, and one that is too
+        small for them raises IndexError where numpy would."""
+        if grid is None:
+            return bool(_effective_actions(self.board, self._device))
+        g = np.asarray(grid)
+        if g.ndim == 2:                                                      # board.py:64-74 promotion
+            g = np.array([g, np.ones_like(g)])
+        R, C = g.shape[1], g.shape[2]
+        if (R, C) == (self.num_rows, self.num_cols):
+            return bool(_effective_actions(g, self._device))
+        eff = set(_effective_actions(g, self._device)) if R * C > 1 else set()
+        for (r1, c1), (r2, c2) in self.action_to_coords:
+            if max(r1, r2) >= R or max(c1, c2) >= C:
+                raise IndexError(f"action {((r1, c1), (r2, c2))} is outside a {R}x{C} grid")
+            a = r1 * C + c1 if c1 == c2 else C * (R - 1) + r1 * (C - 1) + c1      # the grid's own action index
+            if a in eff:
+                return True
+        return False
 
 
 def _effective_actions(board, device=None) -> List[int]:
