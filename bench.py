@@ -263,6 +263,7 @@ def main():
     env.record(ev[2])
     for i in range(args.steps):
         step(args.warmup + i)
+    host_issue_s = time.perf_counter() - t0          # host time to enqueue the window (launch-rate check)
     env.record(ev[3])
     env.join()
     ev[1].record()
@@ -316,6 +317,7 @@ def main():
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(el * 1e3 / args.steps, 4),
+            "host_issue_ms_per_step": round(host_issue_s * 1e3 / args.steps, 4),
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
