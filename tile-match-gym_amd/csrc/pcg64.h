@@ -53,6 +53,61 @@ __host__ __device__ __forceinline__ U128 add128(U128 a, U128 b) {
     return r;
 }
 
+// s = A * f + g (mod 2^128): the jump-ahead s_j = A^j s + G_j inc of a lane
+// (A, g per lane, f = the wave-uniform stream state, in SGPRs).  Device: ten
+// v_mad_u64_u32, whose 64-bit addends carry the next limb's partial sum and
+// whose carry-outs (SGPR masks) are added back with v_addc: the 32-bit limbs
+// r0..r3 of the result are
+//   P = a0 f0 + (g1:g0)            r0 = P.lo                 carry c1 -> r2
+//   Q = a0 f1 + (g2:P.hi)          (at 2^32)                 carry c2 -> r3
+//   R = a1 f0 + Q                  r1 = R.lo                 carry c3 -> r3
+//   S = a0 f2 + (g3:R.hi); T = a1 f1 + S; U = a2 f0 + T   (at 2^64, carries >= 2^128)
+//   r2 = U.lo + c1 (carry c4);  r3 = lo32(U.hi + a0 f3 + a1 f2 + a2 f1 + a3 f0) + c2 + c3 + c4
+// (the compiler's lowering of mul128 + add128 issues 16 multiplies and a
+// dozen moves for the same value).
+#if defined(__HIP_DEVICE_COMPILE__)
+__device__ __forceinline__ uint64_t mad64c(uint32_t a, uint32_t b, uint64_t c, uint64_t &carry) {   // a*b + c, carry out
+    uint64_t d;
+    asm("v_mad_u64_u32 %0, %1, %2, %3, %4" : "=&v"(d), "=s"(carry) : "v"(a), "s"(b), "v"(c));
+    return d;
+}
+__device__ __forceinline__ uint32_t addc32(uint32_t x, uint64_t cin, uint64_t &cout) {                 // x + carry-in bit
+    uint32_t r;
+    asm("v_addc_co_u32_e64 %0, %1, %2, 0, %3" : "=v"(r), "=s"(cout) : "v"(x), "s"(cin));
+    return r;
+}
+#endif
+#ifndef TMG_JUMPASM
+#define TMG_JUMPASM 1          // A/B only (0: mul128 + add128), removed after the measurement
+#endif
+__host__ __device__ __forceinline__ U128 add128(U128 a, U128 b);
+__host__ __device__ __forceinline__ U128 jump128(const U128 &A, const U128 &f, const U128 &g) {
+#if defined(__HIP_DEVICE_COMPILE__) && !TMG_JUMPASM
+    return add128(mul128(A, f), g);
+#elif defined(__HIP_DEVICE_COMPILE__)
+    const uint32_t a0 = (uint32_t)A.lo, a1 = (uint32_t)(A.lo >> 32), a2 = (uint32_t)A.hi, a3 = (uint32_t)(A.hi >> 32);
+    const uint32_t f0 = (uint32_t)f.lo, f1 = (uint32_t)(f.lo >> 32), f2 = (uint32_t)f.hi, f3 = (uint32_t)(f.hi >> 32);
+    uint64_t c1, c2, c3, c4, cx;
+    const uint64_t P = mad64c(a0, f0, g.lo, c1);
+    const uint64_t Q = mad64c(a0, f1, (g.hi << 32) | (P >> 32), c2);
+    const uint64_t R = mad64c(a1, f0, Q, c3);
+    const uint64_t S = mad64c(a0, f2, (g.hi & 0xffffffff00000000ULL) | (R >> 32), cx);
+    const uint64_t T = mad64c(a1, f1, S, cx);
+    const uint64_t U = mad64c(a2, f0, T, cx);
+    const uint32_t r2 = addc32((uint32_t)U, c1, c4);
+    uint64_t W = mad64c(a0, f3, U >> 32, cx);
+    W = mad64c(a1, f2, W, cx);
+    W = mad64c(a2, f1, W, cx);
+    W = mad64c(a3, f0, W, cx);
+    const uint32_t r3 = addc32(addc32(addc32((uint32_t)W, c2, cx), c3, cx), c4, cx);
+    return U128{(R << 32) | (uint32_t)P, ((uint64_t)r3 << 32) | r2};
+#else
+    const unsigned __int128 a = ((unsigned __int128)A.hi << 64) | A.lo, b = ((unsigned __int128)f.hi << 64) | f.lo;
+    const unsigned __int128 s = a * b + (((unsigned __int128)g.hi << 64) | g.lo);
+    return U128{(uint64_t)s, (uint64_t)(s >> 64)};
+#endif
+}
+
 __host__ __device__ __forceinline__ uint64_t xsl_rr(U128 s) {
     uint64_t x = s.hi ^ s.lo;
     unsigned rot = (unsigned)(s.hi >> 58);                 // state >> 122

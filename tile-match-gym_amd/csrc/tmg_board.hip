@@ -33,6 +33,9 @@ namespace tmg {
 constexpr int kLean128Waves = 7;     // step_kernel<128, false>: the c2 / c4 kernel (72 VGPRs)
 constexpr int kGen128Waves = 5;      // step_kernel<128, true>: c3 (96 VGPRs; 6 / 7 spill and lose)
 constexpr int kReset512Waves = 7;    // reset_kernel<512>: c5's regeneration (62 VGPRs: 8 waves)
+#ifndef TMG_C5W
+#define TMG_C5W 4
+#endif
 
 // compiler-only ordering point between a wave's LDS loads and later stores
 #define WFENCE() __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront")
@@ -429,7 +432,7 @@ __device__ __forceinline__ void draw_colours(const Params &P, int lane, const La
     U128 sj{0, 0};
     uint64_t out = 0;
     for (int base = 0; base < n64; base += 64) {
-        sj = add128(mul128(J.Aj, s), J.incG);
+        sj = jump128(J.Aj, s, J.incG);
         out = xsl_rr(sj);
         const int j = base + lane;
         const uint64_t m0 = (uint64_t)(uint32_t)out * k, m1 = (out >> 32) * k;
@@ -606,7 +609,10 @@ __device__ __forceinline__ bool scan_effective_clean(const Params &P, WS &w, int
     };
     uint64_t any = 0;
     for (int base = 0; base < (nv > nh ? nv : nh); base += 64) {
-        const int i = base + lane;
+        // an opaque lane index: the per-lane geometry below stays inside the
+        // pass (with a constant board shape the passes unroll, and values
+        // hoisted out of them would stay live across the callers' loops)
+        const int i = base + loop_lane(lane);
         uint32_t fv, fh;                                     // 0 iff effective
         {   // vertical action i: p = i (top cell), q = p + C
             const int p = i < nv ? i : 0, q = p + C;
@@ -899,9 +905,10 @@ __device__ __forceinline__ void refill(const Params &P, WS &w, int lane, const L
 template <class WS>
 __device__ __forceinline__ void shuffle(const Params &P, WS &w, int lane, Rng &g) {
     const int N = P.N;
+    for (int p = lane; p < N; p += 64) w.u.sh.perm[p] = (int16_t)p;   // arange(R*C), :115
+    WSYNC();
     if (lane == 0) {
         Rng r = g;
-        for (int i = 0; i < N; i++) w.u.sh.perm[i] = (int16_t)i;
         for (int i = N - 1; i >= 1; i--) {
             int j = (int)r_interval(r, (uint32_t)i);
             int16_t x = w.u.sh.perm[i]; w.u.sh.perm[i] = w.u.sh.perm[j]; w.u.sh.perm[j] = x;
@@ -1040,7 +1047,7 @@ __device__ __forceinline__ void bp_ring_init(const Params &P, WS &w, int lane, c
 template <int NB, class WS>
 __device__ __forceinline__ void bp_ring_fill(const Params &P, WS &w, int lane, const LaneJump &J, BpRing &r) {
     const uint32_t k = (uint32_t)P.k;
-    const U128 sj = add128(mul128(J.Aj, r.fs), J.incG);
+    const U128 sj = jump128(J.Aj, r.fs, J.incG);
     const uint64_t out = xsl_rr(sj);
     const uint64_t m0 = (uint64_t)(uint32_t)out * k, m1 = (out >> 32) * k;
     if (P.thr != 0u) {
@@ -1085,7 +1092,7 @@ __device__ __forceinline__ void bp_ring_state(const LaneJump &J, WS &w, const Bp
     const uint32_t *st = bp_slots(w) + 4 * ((i >> 7) & 7);
     const U128 b{((uint64_t)__builtin_amdgcn_readfirstlane(st[1]) << 32) | (uint32_t)__builtin_amdgcn_readfirstlane(st[0]),
                  ((uint64_t)__builtin_amdgcn_readfirstlane(st[3]) << 32) | (uint32_t)__builtin_amdgcn_readfirstlane(st[2])};
-    const U128 sj = add128(mul128(J.Aj, b), J.incG);
+    const U128 sj = jump128(J.Aj, b, J.incG);
     const U128 s{rdlane64(sj.lo, local >> 1), rdlane64(sj.hi, local >> 1)};
     g.slo = s.lo;
     g.shi = s.hi;
@@ -2205,8 +2212,71 @@ __device__ __forceinline__ uint32_t step_env(
 }
 
 // TileMatchEnv.step over a batch, one wave per env.
-template <int MAXN, bool GEN, int SBNB = 0, bool CODD = false>
-__global__ __launch_bounds__(64, MAXN == 128 ? (GEN ? kGen128Waves : kLean128Waves) : 1) void step_kernel(
+// Shape-specialised kernels: for the benchmark shapes the launcher picks an
+// instantiation that tells the compiler the board geometry (R, C, k and what
+// follows from them), so every cell offset, division by C, loop bound and
+// bitboard mask folds to a constant.  The values are asserted to the compiler
+// only; Params still holds them (the host picks the kernel by comparing).
+#if defined(__clang__)
+#define TMG_ASSUME(x) __builtin_assume(x)
+#else
+#define TMG_ASSUME(x) do { if (!(x)) __builtin_unreachable(); } while (0)   // the host wave emulator (g++)
+#endif
+// A fixed shape is encoded as one int, R << 24 | C << 16 | k << 8 | specials
+// mask (0: the generic kernel; specials 255: any, for the reset kernels).
+constexpr int shape_fix(int R, int C, int k, int smask) { return (R << 24) | (C << 16) | (k << 8) | smask; }
+constexpr int kNoFix = 0;
+constexpr int kFixAnySpecials = 255;
+constexpr int kFixC2 = shape_fix(10, 10, 4, 0);                           // BASELINE configs[1] / [3]
+constexpr int kFixC3 = shape_fix(10, 10, 4, SP_VLASER | SP_HLASER | SP_BOMB);   // configs[2]
+constexpr int kFixC5 = shape_fix(20, 20, 6, SP_COOKIE | SP_VLASER | SP_HLASER | SP_BOMB);   // configs[4]
+constexpr int kFixReset10 = shape_fix(10, 10, 4, kFixAnySpecials);
+constexpr int kFixReset20 = shape_fix(20, 20, 6, kFixAnySpecials);
+__host__ __device__ constexpr uint64_t fix_mask(int R, int C, int w, int what) {   // make_params' sb_* masks
+    uint64_t m = 0;
+    for (int p = 0; p < R * C && p < 128; p++) {
+        const int c = p % C;
+        if ((p & 1) != w) continue;
+        const bool on = what == 0 ? true : what == 1 ? p >= C : what == 2 ? p >= 2 * C : what == 3 ? c <= C - 2
+                      : what == 4 ? c >= 1 : c <= C - 3;
+        if (on) m |= 1ULL << (p >> 1);
+    }
+    return m;
+}
+template <int FIX>
+__device__ __forceinline__ void assume_shape(const Params &P) {
+    if constexpr (FIX != kNoFix) {
+        constexpr struct { int R, C, K, smask; } F{FIX >> 24, (FIX >> 16) & 255, (FIX >> 8) & 255, FIX & 255};
+        TMG_ASSUME(P.R == F.R);
+        TMG_ASSUME(P.C == F.C);
+        TMG_ASSUME(P.N == F.R * F.C);
+        TMG_ASSUME(P.A == 2 * F.R * F.C - F.R - F.C);
+        TMG_ASSUME(P.W == (2 * F.R * F.C - F.R - F.C + 63) / 64);
+        TMG_ASSUME(P.k == F.K);
+        if constexpr (F.smask != kFixAnySpecials) TMG_ASSUME(P.smask == F.smask);
+        TMG_ASSUME(P.thr == (F.K > 1 ? (0xffffffffu - (uint32_t)(F.K - 1)) % (uint32_t)F.K : 0u));
+        TMG_ASSUME(P.cmag == ((1u << 20) + (uint32_t)F.C - 1) / (uint32_t)F.C);
+        TMG_ASSUME(P.cm1mag == ((1u << 20) + (uint32_t)F.C - 2) / (uint32_t)(F.C - 1));
+        if constexpr (F.R * F.C <= 128) {
+#define TMG_ASSUME_MASK(field, what)                                          \
+    {                                                                         \
+        constexpr uint64_t m0 = fix_mask(F.R, F.C, 0, what), m1 = fix_mask(F.R, F.C, 1, what); \
+        TMG_ASSUME(P.field[0] == m0);                                   \
+        TMG_ASSUME(P.field[1] == m1);                                   \
+    }
+            TMG_ASSUME_MASK(sb_in, 0)
+            TMG_ASSUME_MASK(sb_u, 1)
+            TMG_ASSUME_MASK(sb_v, 2)
+            TMG_ASSUME_MASK(sb_nl, 3)
+            TMG_ASSUME_MASK(sb_nf, 4)
+            TMG_ASSUME_MASK(sb_h, 5)
+#undef TMG_ASSUME_MASK
+        }
+    }
+}
+
+template <int MAXN, bool GEN, int SBNB = 0, bool CODD = false, int FIX = kNoFix>
+__global__ __launch_bounds__(64, MAXN == 128 ? (GEN ? kGen128Waves : kLean128Waves) : (FIX == kFixC5 ? TMG_C5W : 1)) void step_kernel(
     Params P_, int64_t n, int8_t *__restrict__ board, uint64_t *__restrict__ rng, int32_t *__restrict__ timer,
     const int32_t *__restrict__ actions, int32_t *__restrict__ reward, int32_t *__restrict__ n_new,
     int32_t *__restrict__ n_act, uint8_t *__restrict__ flags_out, uint64_t *__restrict__ eff, int trust_eff,
@@ -2214,6 +2284,7 @@ __global__ __launch_bounds__(64, MAXN == 128 ? (GEN ? kGen128Waves : kLean128Wav
     TMG_SMEM_DECL(smem);
     using WS = Ws<MAXN, GEN>;
     const Params &P = TMG_KERNARG_PARAMS(P_);
+    assume_shape<FIX>(P);
     const int lane = threadIdx.x & 63;
     WS &w = *reinterpret_cast<WS *>(smem);
     const int64_t e = wg_env();
@@ -2294,7 +2365,7 @@ __device__ __forceinline__ void reset_env(const Params &P, WS &w, int lane, int6
     if (lane == 0) timer[e] = 0;
 }
 
-template <int MAXN, int SBNB = 0, bool CODD = false>
+template <int MAXN, int SBNB = 0, bool CODD = false, int FIX = kNoFix>
 __global__ __launch_bounds__(64, MAXN > 128 ? kReset512Waves : 1) void reset_kernel(Params P_, int64_t n, int8_t *__restrict__ board,
                                                              uint64_t *__restrict__ rng, int32_t *__restrict__ timer,
                                                              uint64_t *__restrict__ eff,
@@ -2302,6 +2373,7 @@ __global__ __launch_bounds__(64, MAXN > 128 ? kReset512Waves : 1) void reset_ker
     TMG_SMEM_DECL(smem);
     using WS = Ws<MAXN, false>;
     const Params &P = TMG_KERNARG_PARAMS(P_);
+    assume_shape<FIX>(P);
     const int lane = threadIdx.x & 63;
     WS &w = *reinterpret_cast<WS *>(smem);
     const int64_t e = wg_env();

@@ -10,6 +10,9 @@
 #include "tmg_aux.hip"      // non-template kernels: one TU only
 #endif
 
+#ifndef TMG_FIXSHAPE
+#define TMG_FIXSHAPE 1         // shape-specialised kernels for the benchmark shapes (A/B)
+#endif
 #ifndef TMG_TU
 #error "compile tmg_kernels.hip with -DTMG_TU=1..7"
 #endif
@@ -18,11 +21,17 @@ namespace tmg {
 
 namespace {
 
-template <int MAXN, bool GEN, int NB, bool CODD>
+template <int MAXN, bool GEN, int NB, bool CODD, int FIX = kNoFix>
 void step_one(dim3 grid, hipStream_t s, const Params &P, const StepArgs &a) {
     const size_t lds = sizeof(Ws<MAXN, GEN>);
-    hipLaunchKernelGGL((step_kernel<MAXN, GEN, NB, CODD>), grid, dim3(64), lds, s, P, a.n, a.board, a.rng,
+    hipLaunchKernelGGL((step_kernel<MAXN, GEN, NB, CODD, FIX>), grid, dim3(64), lds, s, P, a.n, a.board, a.rng,
                        a.timer, a.actions, a.reward, a.n_new, a.n_act, a.flags, a.eff, a.trust_eff, a.autoreset);
+}
+// whether P is the shape a FIX instantiation was compiled for
+template <int FIX>
+bool is_shape(const Params &P) {
+    const int sm = (FIX & 255) == kFixAnySpecials ? kFixAnySpecials : P.smask;
+    return TMG_FIXSHAPE && shape_fix(P.R, P.C, P.k, sm) == FIX;
 }
 
 // scalar-bitboard variants: NB colour planes (sb_planes(k))
@@ -43,11 +52,11 @@ void spill_one(hipStream_t s, const Params &P, const StepArgs &a) {
                        a.actions, a.reward, a.n_new, a.n_act, a.flags, a.eff, a.trust_eff, a.autoreset);
 }
 
-template <int MAXN, int NB, bool CODD>
+template <int MAXN, int NB, bool CODD, int FIX = kNoFix>
 void reset_one(dim3 grid, hipStream_t s, const Params &P, int64_t n, int8_t *board, uint64_t *rng, int32_t *timer,
                uint64_t *eff, const uint8_t *env_mask, int mask_bits) {
     const size_t lds = sizeof(Ws<MAXN, false>);
-    hipLaunchKernelGGL((reset_kernel<MAXN, NB, CODD>), grid, dim3(64), lds, s, P, n, board, rng, timer, eff,
+    hipLaunchKernelGGL((reset_kernel<MAXN, NB, CODD, FIX>), grid, dim3(64), lds, s, P, n, board, rng, timer, eff,
                        env_mask, mask_bits);
 }
 
@@ -61,6 +70,7 @@ void effective_one(dim3 grid, hipStream_t s, const Params &P, int64_t n, const i
 
 #if TMG_TU == 1
 void launch_step_lean128(bool sb, dim3 grid, hipStream_t s, const Params &P, const StepArgs &a) {
+    if (sb && is_shape<kFixC2>(P)) { step_one<128, false, 2, false, kFixC2>(grid, s, P, a); return; }
     if (!sb) step_one<128, false, 0, false>(grid, s, P, a);
     else if (P.C & 1) step_sb<false, true>(grid, s, P, a);
     else step_sb<false, false>(grid, s, P, a);
@@ -69,7 +79,8 @@ void launch_step_lean128(bool sb, dim3 grid, hipStream_t s, const Params &P, con
 
 #if TMG_TU == 2
 void launch_step_gen128_even(bool sb, dim3 grid, hipStream_t s, const Params &P, const StepArgs &a) {
-    if (sb) step_sb<true, false>(grid, s, P, a);
+    if (sb && is_shape<kFixC3>(P)) step_one<128, true, 2, false, kFixC3>(grid, s, P, a);
+    else if (sb) step_sb<true, false>(grid, s, P, a);
     else step_one<128, true, 0, false>(grid, s, P, a);
 }
 #endif
@@ -87,13 +98,15 @@ void launch_step_gen128_odd(dim3 grid, hipStream_t s, const Params &P, const Ste
 
 #if TMG_TU == 4
 void launch_step512(bool gen, dim3 grid, hipStream_t s, const Params &P, const StepArgs &a) {
-    if (gen) step_one<512, true, 0, false>(grid, s, P, a);
+    if (gen && is_shape<kFixC5>(P)) step_one<512, true, 0, false, kFixC5>(grid, s, P, a);
+    else if (gen) step_one<512, true, 0, false>(grid, s, P, a);
     else step_one<512, false, 0, false>(grid, s, P, a);
 }
 
 void launch_reset512(dim3 grid, hipStream_t s, const Params &P, int64_t n, int8_t *board, uint64_t *rng,
                      int32_t *timer, uint64_t *eff, const uint8_t *env_mask, int mask_bits) {
     // NB = colour bit-planes of the row-plane generate (bp_generate)
+    if (is_shape<kFixReset20>(P)) { reset_one<512, 3, false, kFixReset20>(grid, s, P, n, board, rng, timer, eff, env_mask, mask_bits); return; }
     switch (sb_planes(P.k)) {
     case 1: reset_one<512, 1, false>(grid, s, P, n, board, rng, timer, eff, env_mask, mask_bits); break;
     case 2: reset_one<512, 2, false>(grid, s, P, n, board, rng, timer, eff, env_mask, mask_bits); break;
@@ -110,6 +123,7 @@ void launch_effective512(dim3 grid, hipStream_t s, const Params &P, int64_t n, c
 void launch_reset128(bool sb, dim3 grid, hipStream_t s, const Params &P, int64_t n, int8_t *board, uint64_t *rng,
                      int32_t *timer, uint64_t *eff, const uint8_t *env_mask, int mask_bits) {
     if (!sb) { reset_one<128, 0, false>(grid, s, P, n, board, rng, timer, eff, env_mask, mask_bits); return; }
+    if (is_shape<kFixReset10>(P)) { reset_one<128, 2, false, kFixReset10>(grid, s, P, n, board, rng, timer, eff, env_mask, mask_bits); return; }
     const bool codd = P.C & 1;
     switch (sb_planes(P.k)) {
     case 1: codd ? reset_one<128, 1, true>(grid, s, P, n, board, rng, timer, eff, env_mask, mask_bits)

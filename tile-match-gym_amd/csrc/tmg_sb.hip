@@ -328,7 +328,7 @@ struct SBDrawPre {
     uint64_t out;
 };
 __device__ __forceinline__ SBDrawPre sb_draw_pre(const LaneJump &J, const Rng &g) {
-    const U128 sj = add128(mul128(J.Aj, U128{g.slo, g.shi}), J.incG);
+    const U128 sj = jump128(J.Aj, U128{g.slo, g.shi}, J.incG);
     return SBDrawPre{sj, xsl_rr(sj)};
 }
 

@@ -242,10 +242,16 @@ struct EmuStep {
     int trust_eff, autoreset;
 };
 
-template <int MAXN, bool GEN, int NB, bool CODD>
+template <int MAXN, bool GEN, int NB, bool CODD, int FIX = tmg::kNoFix>
 static void emu_step_kernel(EmuStep &S) {
     const tmg::Params &P = *S.P;
-    run_blocks(S.n, sizeof(tmg::Ws<MAXN, GEN>), [&] { tmg::step_kernel<MAXN, GEN, NB, CODD>(P, S.n, S.board, S.rng, S.timer, S.actions, S.reward, S.n_new, S.n_act, S.flags, S.eff, S.trust_eff, S.autoreset); });
+    run_blocks(S.n, sizeof(tmg::Ws<MAXN, GEN>), [&] { tmg::step_kernel<MAXN, GEN, NB, CODD, FIX>(P, S.n, S.board, S.rng, S.timer, S.actions, S.reward, S.n_new, S.n_act, S.flags, S.eff, S.trust_eff, S.autoreset); });
+}
+// tmg_kernels.hip's is_shape: the shape-specialised instantiations the launchers pick
+template <int FIX>
+static bool emu_is_shape(const tmg::Params &P) {
+    const int sm = (FIX & 255) == tmg::kFixAnySpecials ? tmg::kFixAnySpecials : P.smask;
+    return tmg::shape_fix(P.R, P.C, P.k, sm) == FIX;
 }
 
 // spill_kernel after a general step launch, as tmg_capi.hip's do_step
@@ -265,10 +271,10 @@ static void emu_step_sb(EmuStep &S) {
     }
 }
 
-template <int MAXN, int NB, bool CODD>
+template <int MAXN, int NB, bool CODD, int FIX = tmg::kNoFix>
 static void emu_reset_kernel(const tmg::Params &P, int64_t n, int8_t *board, uint64_t *rng, int32_t *timer, uint64_t *eff,
                              const uint8_t *mask, int bits) {
-    run_blocks(n, sizeof(tmg::Ws<MAXN, false>), [&] { tmg::reset_kernel<MAXN, NB, CODD>(P, n, board, rng, timer, eff, mask, bits); });
+    run_blocks(n, sizeof(tmg::Ws<MAXN, false>), [&] { tmg::reset_kernel<MAXN, NB, CODD, FIX>(P, n, board, rng, timer, eff, mask, bits); });
 }
 template <bool CODD>
 static void emu_reset_sb(const tmg::Params &P, int64_t n, int8_t *board, uint64_t *rng, int32_t *timer, uint64_t *eff,
@@ -284,7 +290,11 @@ static void emu_reset_sb(const tmg::Params &P, int64_t n, int8_t *board, uint64_
 // as tmg_capi.hip's do_reset
 static void emu_do_reset(const tmg::Params &P, int64_t n, int8_t *board, uint64_t *rng, int32_t *timer, uint64_t *eff,
                          const uint8_t *mask, int bits) {
-    if (sb_ok(P)) {
+    if (emu_is_shape<tmg::kFixReset10>(P)) {
+        emu_reset_kernel<128, 2, false, tmg::kFixReset10>(P, n, board, rng, timer, eff, mask, bits);
+    } else if (emu_is_shape<tmg::kFixReset20>(P)) {
+        emu_reset_kernel<512, 3, false, tmg::kFixReset20>(P, n, board, rng, timer, eff, mask, bits);
+    } else if (sb_ok(P)) {
         if (P.C & 1) emu_reset_sb<true>(P, n, board, rng, timer, eff, mask, bits);
         else emu_reset_sb<false>(P, n, board, rng, timer, eff, mask, bits);
     } else if (P.N <= 128) {
@@ -318,11 +328,13 @@ int emu_step(int R, int C, int k, int smask, int moves, int64_t n, int8_t *board
     if (deferred) S.autoreset = 2;
     if (P.N <= 128) {
         if (lean) {
-            if (!sb_ok(P)) emu_step_kernel<128, false, 0, false>(S);
+            if (sb_ok(P) && emu_is_shape<tmg::kFixC2>(P)) emu_step_kernel<128, false, 2, false, tmg::kFixC2>(S);
+            else if (!sb_ok(P)) emu_step_kernel<128, false, 0, false>(S);
             else if (P.C & 1) emu_step_sb<false, true>(S);
             else emu_step_sb<false, false>(S);
         } else {
-            if (!sb_ok(P)) emu_step_kernel<128, true, 0, false>(S);
+            if (sb_ok(P) && emu_is_shape<tmg::kFixC3>(P)) emu_step_kernel<128, true, 2, false, tmg::kFixC3>(S);
+            else if (!sb_ok(P)) emu_step_kernel<128, true, 0, false>(S);
             else if (P.C & 1) emu_step_sb<true, true>(S);
             else emu_step_sb<true, false>(S);
             emu_spill<128>(S);
@@ -330,7 +342,8 @@ int emu_step(int R, int C, int k, int smask, int moves, int64_t n, int8_t *board
     } else if (lean) {
         emu_step_kernel<512, false, 0, false>(S);
     } else {
-        emu_step_kernel<512, true, 0, false>(S);
+        if (emu_is_shape<tmg::kFixC5>(P)) emu_step_kernel<512, true, 0, false, tmg::kFixC5>(S);
+        else emu_step_kernel<512, true, 0, false>(S);
         emu_spill<512>(S);
     }
     g_spill_total += P.spill->total;
