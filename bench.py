@@ -62,6 +62,21 @@ CONFIGS = {
 }
 
 
+# Profiled run shapes beyond the configs' defaults (tools/issue.py, tools/traffic.py
+# key their counts by these names): c4 = BASELINE configs[3], one GPU's shard of
+# 1 048 576 / 8 boards of the c2 shape.
+PROFILE_RUNS = {"c4": ("c2", 131072)}
+
+
+def profile_key(config, boards):
+    """The profiles/*.json key of a run: its config name, or the PROFILE_RUNS
+    name of its (config, boards)."""
+    for name, (cfg, nb) in PROFILE_RUNS.items():
+        if cfg == config and nb == boards:
+            return name
+    return config
+
+
 def workload_desc(R, C, k, nb, specials):
     """The workload of a run as it was actually configured (--boards included)."""
     return f"{nb} x {R}x{C} boards per GPU, {k} colours, {specials}"
@@ -144,7 +159,7 @@ def load_profile(name, config, boards, groups):
         return None
     try:
         with open(p) as f:
-            prof = json.load(f).get(config)
+            prof = json.load(f).get(profile_key(config, boards))
     except Exception:
         return None
     if not prof or prof.get("boards_per_gpu") != boards or prof.get("env_groups_per_gpu") != groups:

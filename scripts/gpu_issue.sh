@@ -6,8 +6,10 @@ cd "${GRAFT_REPO_ROOT:-/root/repo}"
 mkdir -p gpurun_out/issue gpurun_out/traffic gpurun_out/stats
 export TMPDIR=/tmp
 S=${STEPS:-60}; W=${WARMUP:-30}
-for cfg in ${CONFIGS:-c2 c3 c5}; do
-  ARGS="--config $cfg --steps $S --warmup $W --no-cpu-baseline"
+# bench arguments of a config name (c4: BASELINE configs[3], one GPU's shard; bench.PROFILE_RUNS)
+bargs() { case $1 in c4) echo "--config c2 --boards 131072";; *) echo "--config $1";; esac; }
+for cfg in ${CONFIGS:-c2 c3 c5 c4}; do
+  ARGS="$(bargs $cfg) --steps $S --warmup $W --no-cpu-baseline"
   timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/stats/$cfg -o run --output-format csv \
     -- python3 bench.py $ARGS > gpurun_out/stats/$cfg.log 2>&1 || { echo "stats $cfg failed"; tail -5 gpurun_out/stats/$cfg.log; exit 1; }
   echo "stats $cfg ok: $(tail -1 gpurun_out/stats/$cfg.log | cut -c1-160)"
@@ -23,4 +25,4 @@ for cfg in ${CONFIGS:-c2 c3 c5}; do
   done
 done
 python3 tools/issue.py gpurun_out/issue $((S + W)) > gpurun_out/issue.json && cat gpurun_out/issue.json
-python3 tools/traffic.py gpurun_out/traffic > gpurun_out/traffic.json && cat gpurun_out/traffic.json
+python3 tools/traffic.py gpurun_out/traffic $((S + W)) > gpurun_out/traffic.json && cat gpurun_out/traffic.json

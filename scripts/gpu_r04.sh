@@ -14,6 +14,8 @@ OUT=gpurun_out/$TAG
 mkdir -p $OUT
 export TMPDIR=/tmp
 PYT="python -u -m pytest -x -v --timeout 240 --timeout-method thread"
+# bench arguments of a config name (c4: BASELINE configs[3], one GPU's shard of 1 048 576 / 8 boards)
+bargs() { case $1 in c4) echo "--config c2 --boards 131072";; *) echo "--config $1";; esac; }
 case "${STAGE:-tests}" in
 tests)
   TMG_EVIDENCE_DIR=$OUT/evidence timeout -k 10 900 $PYT tests -m gpu --ignore=tests/test_gpu_deep.py \
@@ -31,8 +33,8 @@ deep)
   tail -3 $OUT/pytest_deep.log
   ;;
 bench)
-  for c in c2 c3 c5; do
-    timeout -k 10 400 python bench.py --config $c > $OUT/${c}_bench.log 2>&1 || { echo "bench $c failed"; tail $OUT/${c}_bench.log; exit 1; }
+  for c in ${CONFIGS:-c2 c3 c5 c4}; do
+    timeout -k 10 400 python bench.py $(bargs $c) > $OUT/${c}_bench.log 2>&1 || { echo "bench $c failed"; tail $OUT/${c}_bench.log; exit 1; }
     tail -1 $OUT/${c}_bench.log | cut -c1-200
   done
   timeout -k 10 300 python bench.py --steps 20 --warmup 5 --no-cpu-baseline > $OUT/c2_driver_window_bench.log 2>&1 || exit 1
@@ -104,22 +106,13 @@ pmcmb)
   done
   done
   ;;
-stamps)
-  # per-env phase durations from the TMG_STAMPS diagnostic build (make ... VARIANT=stamps STAMPS=1)
-  for c in ${CONFIGS:-c2}; do
-    TMG_LIB=$PWD/tile-match-gym_amd/tile_match_gym_amd/_lib/libtmg_stamps.so timeout -k 10 240 \
-      python tools/stamps.py --config $c --steps 60 > $OUT/${c}_stamps.log 2>&1 \
-      || { echo "stamps $c failed"; tail $OUT/${c}_stamps.log; exit 1; }
-    tail -8 $OUT/${c}_stamps.log
-  done
-  ;;
 all)
   STAGE=tests bash scripts/gpu_r04.sh && STAGE=deep bash scripts/gpu_r04.sh && STAGE=bench bash scripts/gpu_r04.sh
   ;;
 prof)
-  for c in ${CONFIGS:-c2 c3 c5}; do
+  for c in ${CONFIGS:-c2 c3 c5 c4}; do
     timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $OUT/prof_$c -o run --output-format csv -- \
-      python3 bench.py --config $c --steps 90 --warmup 30 --no-cpu-baseline > $OUT/${c}_prof_bench.log 2>&1 \
+      python3 bench.py $(bargs $c) --steps 90 --warmup 30 --no-cpu-baseline > $OUT/${c}_prof_bench.log 2>&1 \
       || { echo "prof $c failed"; tail $OUT/${c}_prof_bench.log; exit 1; }
     tail -1 $OUT/${c}_prof_bench.log | cut -c1-200
   done

@@ -77,14 +77,9 @@ __device__ __forceinline__ uint32_t addc32(uint32_t x, uint64_t cin, uint64_t &c
     return r;
 }
 #endif
-#ifndef TMG_JUMPASM
-#define TMG_JUMPASM 1          // A/B only (0: mul128 + add128), removed after the measurement
-#endif
 __host__ __device__ __forceinline__ U128 add128(U128 a, U128 b);
 __host__ __device__ __forceinline__ U128 jump128(const U128 &A, const U128 &f, const U128 &g) {
-#if defined(__HIP_DEVICE_COMPILE__) && !TMG_JUMPASM
-    return add128(mul128(A, f), g);
-#elif defined(__HIP_DEVICE_COMPILE__)
+#if defined(__HIP_DEVICE_COMPILE__)
     const uint32_t a0 = (uint32_t)A.lo, a1 = (uint32_t)(A.lo >> 32), a2 = (uint32_t)A.hi, a3 = (uint32_t)(A.hi >> 32);
     const uint32_t f0 = (uint32_t)f.lo, f1 = (uint32_t)(f.lo >> 32), f2 = (uint32_t)f.hi, f3 = (uint32_t)(f.hi >> 32);
     uint64_t c1, c2, c3, c4, cx;

@@ -33,9 +33,7 @@ namespace tmg {
 constexpr int kLean128Waves = 7;     // step_kernel<128, false>: the c2 / c4 kernel (72 VGPRs)
 constexpr int kGen128Waves = 5;      // step_kernel<128, true>: c3 (96 VGPRs; 6 / 7 spill and lose)
 constexpr int kReset512Waves = 7;    // reset_kernel<512>: c5's regeneration (62 VGPRs: 8 waves)
-#ifndef TMG_C5W
-#define TMG_C5W 4
-#endif
+constexpr int kC5StepWaves = 4;      // step_kernel<512, true> specialised for c5 (128 VGPRs; 3 measured the same)
 
 // compiler-only ordering point between a wave's LDS loads and later stores
 #define WFENCE() __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront")
@@ -2276,7 +2274,7 @@ __device__ __forceinline__ void assume_shape(const Params &P) {
 }
 
 template <int MAXN, bool GEN, int SBNB = 0, bool CODD = false, int FIX = kNoFix>
-__global__ __launch_bounds__(64, MAXN == 128 ? (GEN ? kGen128Waves : kLean128Waves) : (FIX == kFixC5 ? TMG_C5W : 1)) void step_kernel(
+__global__ __launch_bounds__(64, MAXN == 128 ? (GEN ? kGen128Waves : kLean128Waves) : (FIX == kFixC5 ? kC5StepWaves : 1)) void step_kernel(
     Params P_, int64_t n, int8_t *__restrict__ board, uint64_t *__restrict__ rng, int32_t *__restrict__ timer,
     const int32_t *__restrict__ actions, int32_t *__restrict__ reward, int32_t *__restrict__ n_new,
     int32_t *__restrict__ n_act, uint8_t *__restrict__ flags_out, uint64_t *__restrict__ eff, int trust_eff,

@@ -10,9 +10,6 @@
 #include "tmg_aux.hip"      // non-template kernels: one TU only
 #endif
 
-#ifndef TMG_FIXSHAPE
-#define TMG_FIXSHAPE 1         // shape-specialised kernels for the benchmark shapes (A/B)
-#endif
 #ifndef TMG_TU
 #error "compile tmg_kernels.hip with -DTMG_TU=1..7"
 #endif
@@ -31,7 +28,7 @@ void step_one(dim3 grid, hipStream_t s, const Params &P, const StepArgs &a) {
 template <int FIX>
 bool is_shape(const Params &P) {
     const int sm = (FIX & 255) == kFixAnySpecials ? kFixAnySpecials : P.smask;
-    return TMG_FIXSHAPE && shape_fix(P.R, P.C, P.k, sm) == FIX;
+    return shape_fix(P.R, P.C, P.k, sm) == FIX;
 }
 
 // scalar-bitboard variants: NB colour planes (sb_planes(k))

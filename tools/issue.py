@@ -40,8 +40,9 @@ def main():
     root, steps = sys.argv[1], int(sys.argv[2])
     out = {}
     for d in sorted(glob.glob(os.path.join(root, "c*"))):
-        cfg = os.path.basename(d)
-        if cfg not in bench.CONFIGS:
+        name = os.path.basename(d)                          # a config or a bench.PROFILE_RUNS name
+        cfg, run_boards = bench.PROFILE_RUNS.get(name, (name, 0))
+        if cfg not in bench.CONFIGS or not os.path.isdir(d):
             continue
         names, rows = per_dispatch(d)
         order = sorted(names)
@@ -60,9 +61,9 @@ def main():
                 continue
             for c, v in rows[i].items():
                 tot[c] += v
-        boards = int(os.environ.get("BOARDS", "0")) or bench.CONFIGS[cfg][5]   # bench --boards of the profiled runs
+        boards = run_boards or bench.CONFIGS[cfg][5]           # bench --boards of the profiled run
         env_steps = steps * boards
-        out[cfg] = {
+        out[name] = {
             "valu_per_env_step": round(tot["SQ_INSTS_VALU"] / env_steps, 2),
             "salu_per_env_step": round(tot["SQ_INSTS_SALU"] / env_steps, 2),
             "lds_per_env_step": round(tot["SQ_INSTS_LDS"] / env_steps, 2),
@@ -71,10 +72,11 @@ def main():
             "env_steps": env_steps,
             # the bench run these counts belong to (bench.py attaches them only to a line of the same run shape)
             "boards_per_gpu": boards,
-            "env_groups_per_gpu": int(os.environ.get("GROUPS", "3")),
+            "env_groups_per_gpu": 3,
             "dispatches": {"step_kernel": n_step, "reset_kernel": n_reset},
-            "source": f"rocprofv3 --pmc {' '.join(COUNTERS)} --kernel-trace, bench.py --config {cfg} "
-                      f"(steps + warmup = {steps}); scripts/gpu_issue.sh, tools/issue.py",
+            "source": (f"rocprofv3 --pmc {' '.join(COUNTERS)} --kernel-trace, bench.py --config {cfg} "
+                       + (f"--boards {boards} " if run_boards else "")
+                       + f"(steps + warmup = {steps}); scripts/gpu_issue.sh, tools/issue.py"),
         }
     json.dump(out, sys.stdout, indent=1)
     print()
