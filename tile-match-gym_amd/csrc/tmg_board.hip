@@ -1037,30 +1037,51 @@ __device__ __forceinline__ void bp_ring_init(const Params &P, WS &w, int lane, c
     r.cons0 = r.cons;
 }
 
+// The batch's lane order: lane l computes PCG64 output bp_out(l) of the batch
+// (outputs o and 32 + o on lanes 2o and 2o + 1), so that the codes of colours l
+// and 64 + l (output l >> 1 resp. 32 + (l >> 1), half l & 1) are on lane l or
+// its quad neighbour l ^ 1: one DPP swap each instead of a cross-lane gather.
+// Output 63, the next batch's starting state, stays on lane 63.
+__device__ __forceinline__ int bp_out(int lane) { return (lane >> 1) + ((lane & 1) << 5); }
+__device__ __forceinline__ int bp_lane(int out) { return out < 32 ? 2 * out : 2 * (out - 32) + 1; }   // inverse
+// A^{bp_out(lane)+1} and G_{bp_out(lane)+1} * inc (the LaneJump fields the fill uses)
+struct BpJump {
+    U128 Aj, incG;
+};
+__device__ __forceinline__ BpJump load_bp_jump(const Params &P, int lane, const Rng &g) {
+    const uint64_t *t = P.jump + bp_out(lane) * 4;
+    return BpJump{U128{t[0], t[1]}, mul128(U128{g.ilo, g.ihi}, U128{t[2], t[3]})};
+}
+
 // the next 128 colours (64 PCG64 outputs by jump-ahead, Lemire-32 on each
-// half) appended to the plane strings: lane l fetches the codes of colours l
-// and 64 + l (output l >> 1, half l & 1), and one ballot per plane and half
+// half) appended to the plane strings: lane l gets the codes of colours l and
+// 64 + l from itself and its quad neighbour, and one ballot per plane and half
 // gives the batch's bits in sequence order; lane 0 stores them and the
 // batch's starting state
 template <int NB, class WS>
-__device__ __forceinline__ void bp_ring_fill(const Params &P, WS &w, int lane, const LaneJump &J, BpRing &r) {
+__device__ __forceinline__ void bp_ring_fill(const Params &P, WS &w, int lane, const BpJump &J, BpRing &r) {
     const uint32_t k = (uint32_t)P.k;
     const U128 sj = jump128(J.Aj, r.fs, J.incG);
     const uint64_t out = xsl_rr(sj);
     const uint64_t m0 = (uint64_t)(uint32_t)out * k, m1 = (out >> 32) * k;
     if (P.thr != 0u) {
-        const bool rj = ((uint32_t)m0 < P.thr) | ((uint32_t)m1 < P.thr);
-        if (__ballot(rj) != 0ULL) r.rej = true;
+        if (__ballot(umin((uint32_t)m0, (uint32_t)m1) < P.thr) != 0ULL) r.rej = true;
     }
-    const int pk = (int)((m0 >> 32) | ((m1 >> 32) << 4));       // codes of colours 2*lane, 2*lane+1
-    const int sh = (lane & 1) << 2;
-    const int x0 = __builtin_amdgcn_ds_bpermute((lane >> 1) << 2, pk) >> sh;
-    const int x1 = __builtin_amdgcn_ds_bpermute((32 + (lane >> 1)) << 2, pk) >> sh;
+    const uint32_t c0 = (uint32_t)(m0 >> 32), c1 = (uint32_t)(m1 >> 32);   // codes of colours 2o, 2o + 1
+    const uint32_t n0 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)c0, 0xb1, 0xf, 0xf, true);   // quad_perm [1,0,3,2]
+    const uint32_t n1 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)c1, 0xb1, 0xf, 0xf, true);
+    const bool odd = lane & 1;
+    const uint32_t x0 = odd ? n1 : c0, x1 = odd ? c1 : n0;        // codes of colours l, 64 + l (< 2^NB)
     uint64_t b0[NB], b1[NB];
 #pragma unroll
     for (int b = 0; b < NB; b++) {
-        b0[b] = __ballot((x0 >> b) & 1);
-        b1[b] = __ballot((x1 >> b) & 1);
+        if (b == NB - 1) {                                        // the top bit: one compare
+            b0[b] = __ballot(x0 >= (1u << b));
+            b1[b] = __ballot(x1 >= (1u << b));
+        } else {
+            b0[b] = __ballot((x0 >> b) & 1u);
+            b1[b] = __ballot((x1 >> b) & 1u);
+        }
     }
     const int q = (r.fill >> 5) & (kBpRingDw - 1);
     if (lane == 0) {
@@ -1083,7 +1104,7 @@ __device__ __forceinline__ void bp_ring_fill(const Params &P, WS &w, int lane, c
 // The exact PCG64 state after the last consumed colour: lane L of the batch
 // holding it, recomputed from that batch's starting state (its LDS slot).
 template <class WS>
-__device__ __forceinline__ void bp_ring_state(const LaneJump &J, WS &w, const BpRing &r, Rng &g) {
+__device__ __forceinline__ void bp_ring_state(const BpJump &J, WS &w, const BpRing &r, Rng &g) {
     if (r.cons == r.cons0) return;                                   // nothing taken since bp_ring_init(g)
     const int i = r.cons - 1, local = i & 127;                       // i >= 128: a take draws >= 2 colours
     WSYNC();
@@ -1091,7 +1112,8 @@ __device__ __forceinline__ void bp_ring_state(const LaneJump &J, WS &w, const Bp
     const U128 b{((uint64_t)__builtin_amdgcn_readfirstlane(st[1]) << 32) | (uint32_t)__builtin_amdgcn_readfirstlane(st[0]),
                  ((uint64_t)__builtin_amdgcn_readfirstlane(st[3]) << 32) | (uint32_t)__builtin_amdgcn_readfirstlane(st[2])};
     const U128 sj = jump128(J.Aj, b, J.incG);
-    const U128 s{rdlane64(sj.lo, local >> 1), rdlane64(sj.hi, local >> 1)};
+    const int l = bp_lane(local >> 1);
+    const U128 s{rdlane64(sj.lo, l), rdlane64(sj.hi, l)};
     g.slo = s.lo;
     g.shi = s.hi;
     g.h = ((uint64_t)((local & 1) ^ 1) << 32) | (uint32_t)(xsl_rr(s) >> 32);   // lo half taken: hi half buffered
@@ -1099,7 +1121,7 @@ __device__ __forceinline__ void bp_ring_state(const LaneJump &J, WS &w, const Bp
 
 // rows 0..row <- the ring's next (row + 1) * C colours (colour plane only)
 template <int NB, class WS>
-__device__ __forceinline__ void bp_take(const Params &P, WS &w, int lane, const LaneJump &J, BpRing &r, int row,
+__device__ __forceinline__ void bp_take(const Params &P, WS &w, int lane, const BpJump &J, BpRing &r, int row,
                                         uint32_t cm, RowPlanes<NB> &pl) {
     const int M = (row + 1) * P.C;
     while (r.fill - r.cons < M) bp_ring_fill<NB>(P, w, lane, J, r);
@@ -1183,9 +1205,10 @@ __device__ __forceinline__ RowPlanes<NB> bp_from_lds(const Params &P, const WS &
 // state and the caller redoes the board on an exact draw-by-draw path.
 // Leaves the board in LDS (colour plane; types 1) and its mask in w.effw.
 template <int NB, class WS>
-__device__ __forceinline__ int bp_generate(const Params &P, WS &w, int lane, const LaneJump &J, Rng &g) {
+__device__ __forceinline__ int bp_generate(const Params &P, WS &w, int lane, Rng &g) {
     const int R = P.R, C = P.C, N = P.N;
     const Rng g0 = g;
+    const BpJump J = load_bp_jump(P, lane, g);
     const uint32_t cm = C >= 32 ? ~0u : (1u << C) - 1u;
     const uint32_t hml = (lane < R && C >= 3) ? cm >> 2 : 0u;          // columns <= C-3
     const uint32_t vml = (lane >= 2 && lane < R) ? cm : 0u;            // rows >= 2
@@ -2171,7 +2194,7 @@ __device__ __forceinline__ uint32_t step_env(
             if (autoreset == 1) {
                 int fg = -1;
                 if constexpr (SBNB > 0) {
-                    if (P.C <= 32) fg = bp_generate<SBNB>(P, w, lane, J, g);
+                    if (P.C <= 32) fg = bp_generate<SBNB>(P, w, lane, g);
                     if (fg < 0) fg = sb_generate_exact<SBNB, CODD>(P, w, lane, J, g, cl);
                 } else {
                     fg = generate_board(P, w, lane, J, g, cl);
@@ -2343,15 +2366,15 @@ __device__ __forceinline__ void reset_env(const Params &P, WS &w, int lane, int6
                                           uint64_t *__restrict__ eff) {
     const int N = P.N, W = P.W;
     Rng g = load_rng(rng + e * 5);
-    const LaneJump J = load_jump(P, lane, g);
     const Cells<MAXN / 64> cl = make_cells<MAXN / 64>(P, lane);
     // board.py:95-109: on row bit-planes (C <= 32); a Lemire rejection or a
     // wider board takes the exact draw-by-draw path
     int fl = -1;
     if constexpr (SBNB > 0) {
-        if (P.C <= 32) fl = bp_generate<SBNB>(P, w, lane, J, g);
+        if (P.C <= 32) fl = bp_generate<SBNB>(P, w, lane, g);
     }
     if (fl < 0) {
+        const LaneJump J = load_jump(P, lane, g);
         if constexpr (MAXN == 128 && SBNB > 0) fl = sb_generate_exact<SBNB, CODD>(P, w, lane, J, g, cl);
         else fl = generate_board(P, w, lane, J, g, cl);
     }

@@ -162,7 +162,8 @@ static void run_wave(void (*body)(void *), void *arg) {
                 const uint32_t old = (uint32_t)(g_lanes[l].val >> 32);
                 const int row = l >> 4, bank = (l & 15) >> 2;
                 int srcl = -1;
-                if (ctrl >= 0x111 && ctrl <= 0x11f) { int n = ctrl - 0x110; if ((l & 15) >= n) srcl = l - n; }
+                if (ctrl <= 0xff) srcl = (l & ~3) | ((ctrl >> (2 * (l & 3))) & 3);       // quad_perm
+                else if (ctrl >= 0x111 && ctrl <= 0x11f) { int n = ctrl - 0x110; if ((l & 15) >= n) srcl = l - n; }
                 else if (ctrl == 0x138) { if (l >= 1) srcl = l - 1; }                 // wave_shr:1
                 else if (ctrl == 0x130) { if (l <= 62) srcl = l + 1; }                // wave_shl:1
                 else if (ctrl == 0x142) { if (row >= 1) srcl = row * 16 - 1; }
