@@ -36,13 +36,18 @@ typedef const TMG_CONST_AS uint64_t sbrow_t;
 #ifndef TMG_KEEP_V3
 #define TMG_KEEP_V3(x, y, z) asm volatile("" ::"v"(x), "v"(y), "v"(z))
 #endif
-__device__ __forceinline__ Pair sb_row(const Params &P, int r) {           // cells of row r
-    const sbrow_t *t = (const sbrow_t *)P.sb_rows + 4 * r;
-    return Pair{t[0], t[1]};
-}
-__device__ __forceinline__ Pair sb_rows_to(const Params &P, int r) {       // cells of rows 0..r
-    const sbrow_t *t = (const sbrow_t *)P.sb_rows + 4 * r;
-    return Pair{t[2], t[3]};
+// cells of row r.  Even C: row r is bits [rC/2, rC/2 + C/2) of both words,
+// two SALU ops instead of two dependent scalar loads in the cascade loop.
+template <bool CODD>
+__device__ __forceinline__ Pair sb_row(const Params &P, int r) {
+    if constexpr (!CODD) {
+        const int h = P.C >> 1;
+        const uint64_t m = lowmask(h) << (r * h);
+        return Pair{m, m};
+    } else {
+        const sbrow_t *t = (const sbrow_t *)P.sb_rows + 4 * r;
+        return Pair{t[0], t[1]};
+    }
 }
 
 // fwd: result[q] = x[q - d] (content moves d cells forward); bwd: result[q] =
@@ -170,7 +175,7 @@ __device__ __forceinline__ void sb_line_keys(const Params &P, int lane, int &key
 template <bool CODD>
 __device__ __forceinline__ void sb_coords(const Params &P, const SBDet &d, int rs, Pair &kh, Pair &kv) {
     const int C = P.C;
-    const Pair row = sb_row(P, rs);
+    const Pair row = sb_row<CODD>(P, rs);
     const Pair eqU = andn(Pair{P.sb_u[0], P.sb_u[1]}, d.neU);      // same colour as the cell above
     const Pair h = d.ha & row;
     kh = h | fwd<true>(h, 1) | fwd<false>(h, 2);
@@ -488,7 +493,7 @@ __device__ __forceinline__ int sb_simple_step(const Params &P, WS &w, int lane, 
     const int rs = sb_bottom_row(P, d);
     if (rs < 0) return -1;
     const int S = P.smask;
-    const Pair row = sb_row(P, rs);
+    const Pair row = sb_row<CODD>(P, rs);
     const Pair eqU = andn(Pair{P.sb_u[0], P.sb_u[1]}, d.neU);
     // first-pass line lengths: a horizontal run of L cells holds L-2 anchors
     const Pair h = d.ha & row;
@@ -639,7 +644,7 @@ __device__ __forceinline__ int sb_simple_step(const Params &P, WS &w, int lane, 
                 }
                 area = area & inb;
             } else if (nonzero(bit & hls)) {                               // h-laser: row r
-                area = sb_row(P, r);
+                area = sb_row<CODD>(P, r);
             } else {                                                       // bomb: 3x3
                 area = Pair{0, 0};
                 for (int i = r > 0 ? r - 1 : 0; i <= (r + 1 < P.R ? r + 1 : P.R - 1); i++)
