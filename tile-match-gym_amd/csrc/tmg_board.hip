@@ -1084,7 +1084,33 @@ __device__ __forceinline__ void bp_ring_fill(const Params &P, WS &w, int lane, c
         }
     }
     const int q = (r.fill >> 5) & (kBpRingDw - 1);
-    if (lane == 0) {
+    if constexpr (WS::NP > 2) {
+        // 512-cell kernels: one VGPR base (ring + q) for every store.  The
+        // planes, their guard copies and the batch's state slot (bp_slots +
+        // 4 * (fill >> 7 & 7) = ring + 144 + q) sit at immediate offsets from
+        // it, where separate scalar bases each needed a v_mov.  (In the 128-cell
+        // lean kernel's inline autoreset this form costs a VGPR, and a wave.)
+        uint32_t *ws = reinterpret_cast<uint32_t *>(&w);
+        int at = (int)(bp_ring(w) - ws) + q;                         // dword index of ring + q (scalar)
+        TMG_OPAQUE_V(at);
+        if (lane == 0) {
+            uint64_t *d = reinterpret_cast<uint64_t *>(ws + at);
+#pragma unroll
+            for (int b = 0; b < NB; b++) {
+                d[b * kBpPlaneDw / 2] = b0[b];
+                d[b * kBpPlaneDw / 2 + 1] = b1[b];
+            }
+            if (q == 0) {                                            // guard copy
+#pragma unroll
+                for (int b = 0; b < NB; b++) {
+                    d[b * kBpPlaneDw / 2 + kBpRingDw / 2] = b0[b];
+                    d[b * kBpPlaneDw / 2 + kBpRingDw / 2 + 1] = b1[b];
+                }
+            }
+            d[2 * kBpPlaneDw] = r.fs.lo;                             // 4 * kBpPlaneDw dwords on
+            d[2 * kBpPlaneDw + 1] = r.fs.hi;
+        }
+    } else if (lane == 0) {
         uint32_t *ring = bp_ring(w);
 #pragma unroll
         for (int b = 0; b < NB; b++) {

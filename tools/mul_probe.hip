@@ -95,6 +95,41 @@ __global__ void k_lshl_add64(uint32_t *out, uint32_t seed) {
     out[blockIdx.x * blockDim.x + threadIdx.x] = (uint32_t)(r ^ (r >> 32));
 }
 
+
+// one-operand-pair 32-bit forms: v = op(v, m)
+#define K32(NAME, ASM)                                                                  \
+    __global__ void NAME(uint32_t *out, uint32_t seed) {                                \
+        uint32_t v[8];                                                                  \
+        for (int i = 0; i < 8; i++) v[i] = threadIdx.x * 7 + i + seed;                  \
+        const uint32_t m = seed | 1;                                                    \
+        for (int it = 0; it < ITER; it++) {                                             \
+            _Pragma("unroll") for (int i = 0; i < 8; i++) asm volatile(ASM : "+v"(v[i]) : "v"(m)); \
+        }                                                                               \
+        uint32_t r = 0;                                                                 \
+        for (int i = 0; i < 8; i++) r ^= v[i];                                          \
+        out[blockIdx.x * blockDim.x + threadIdx.x] = r;                                 \
+    }
+K32(k_alignbit, "v_alignbit_b32 %0, %0, %1, %1")
+K32(k_bfe, "v_bfe_u32 %0, %0, %1, 1")
+K32(k_dpp, "v_mov_b32_dpp %0, %0 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf")
+K32(k_cndmask, "v_cndmask_b32 %0, %0, %1, vcc")
+K32(k_xor, "v_xor_b32 %0, %0, %1")
+
+#define K64(NAME, ASM)                                                                  \
+    __global__ void NAME(uint32_t *out, uint32_t seed) {                                \
+        uint64_t v[8];                                                                  \
+        for (int i = 0; i < 8; i++) v[i] = threadIdx.x * 7 + i + seed;                  \
+        const uint32_t m = (seed | 1) & 31;                                             \
+        for (int it = 0; it < ITER; it++) {                                             \
+            _Pragma("unroll") for (int i = 0; i < 8; i++) asm volatile(ASM : "+v"(v[i]) : "v"(m)); \
+        }                                                                               \
+        uint64_t r = 0;                                                                 \
+        for (int i = 0; i < 8; i++) r ^= v[i];                                          \
+        out[blockIdx.x * blockDim.x + threadIdx.x] = (uint32_t)(r ^ (r >> 32));         \
+    }
+K64(k_lshl64, "v_lshlrev_b64 %0, %1, %0")
+K64(k_mov64, "v_mov_b64 %0, %0")
+
 int main() {
     int dev = 0;
     hipDeviceProp_t p;
@@ -106,7 +141,10 @@ int main() {
     hipMalloc(&out, (size_t)blocks * 64 * 4);
     struct K { const char *name; void (*f)(uint32_t *, uint32_t); };
     K ks[] = {{"v_add_u32", k_add}, {"v_mul_lo_u32", k_mul_lo}, {"v_mul_hi_u32", k_mul_hi},
-              {"v_mul_u32_u24", k_mul_u24}, {"v_mad_u64_u32", k_mad64}, {"v_lshl_add_u64", k_lshl_add64}};
+              {"v_mul_u32_u24", k_mul_u24}, {"v_mad_u64_u32", k_mad64}, {"v_lshl_add_u64", k_lshl_add64},
+              {"v_alignbit_b32", k_alignbit}, {"v_bfe_u32", k_bfe}, {"v_mov_b32_dpp", k_dpp},
+              {"v_cndmask_b32", k_cndmask}, {"v_xor_b32", k_xor}, {"v_lshlrev_b64", k_lshl64},
+              {"v_mov_b64", k_mov64}};
     hipEvent_t a, b;
     hipEventCreate(&a);
     hipEventCreate(&b);
