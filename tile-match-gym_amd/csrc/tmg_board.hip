@@ -32,7 +32,12 @@ namespace tmg {
 // kernel; each measured on the MI355X against its neighbours.
 constexpr int kLean128Waves = 7;     // step_kernel<128, false>: the c2 / c4 kernel (72 VGPRs)
 constexpr int kGen128Waves = 5;      // step_kernel<128, true>: c3 (96 VGPRs; 6 / 7 spill and lose)
-constexpr int kReset512Waves = 7;    // reset_kernel<512>: c5's regeneration (62 VGPRs: 8 waves)
+constexpr int kReset512Waves = 7;    // reset_kernel<512>: c5's regeneration
+constexpr int kReset128Waves = 8;    // reset_kernel<128> specialised for 10x10 k4 (c3): 63 VGPRs
+#ifndef TMG_MRE
+#define TMG_MRE 2
+#endif
+constexpr int kMaskedResetEnvs = TMG_MRE;   // envs per wave of a masked reset_kernel launch
 constexpr int kC5StepWaves = 4;      // step_kernel<512, true> specialised for c5 (128 VGPRs; 3 measured the same)
 
 // compiler-only ordering point between a wave's LDS loads and later stores
@@ -2413,20 +2418,30 @@ __device__ __forceinline__ void reset_env(const Params &P, WS &w, int lane, int6
 }
 
 template <int MAXN, int SBNB = 0, bool CODD = false, int FIX = kNoFix>
-__global__ __launch_bounds__(64, MAXN > 128 ? kReset512Waves : 1) void reset_kernel(Params P_, int64_t n, int8_t *__restrict__ board,
+__global__ __launch_bounds__(64, MAXN > 128 ? kReset512Waves : (FIX != kNoFix ? kReset128Waves : 1)) void reset_kernel(Params P_, int64_t n, int8_t *__restrict__ board,
                                                              uint64_t *__restrict__ rng, int32_t *__restrict__ timer,
                                                              uint64_t *__restrict__ eff,
-                                                             const uint8_t *__restrict__ env_mask, int mask_bits) {
+                                                             const uint8_t *__restrict__ env_mask, int mask_bits,
+                                                             int epw) {
     TMG_SMEM_DECL(smem);
     using WS = Ws<MAXN, false>;
     const Params &P = TMG_KERNARG_PARAMS(P_);
     assume_shape<FIX>(P);
     const int lane = threadIdx.x & 63;
     WS &w = *reinterpret_cast<WS *>(smem);
-    const int64_t e = wg_env();
-    if (e >= n) return;
-    if (env_mask && !(__builtin_amdgcn_readfirstlane((int)env_mask[e]) & mask_bits)) return;
-    reset_env<MAXN, SBNB, CODD>(P, w, lane, e, board, rng, timer, eff);
+    // epw consecutive envs per wave (1 for a full reset; a masked reset, where
+    // most launches find nothing to do, dispatches epw times fewer waves and
+    // regenerates the envs it finds one after another)
+    const int64_t e0 = wg_env() * epw;
+    if (e0 >= n) return;
+    const int64_t el = e0 + lane;
+    uint64_t todo = __ballot(lane < epw && el < n && (!env_mask || (env_mask[el] & mask_bits)));
+    while (todo) {
+        const int k = __builtin_ctzll(todo);
+        todo &= todo - 1;
+        reset_env<MAXN, SBNB, CODD>(P, w, loop_lane(lane), e0 + k, board, rng, timer, eff);
+        WSYNC();                                                         // the next board reuses the workspace
+    }
 }
 
 // TileMatchEnv._get_effective_actions for arbitrary boards (tile_match_env.py:118-124)

@@ -51,10 +51,10 @@ void spill_one(hipStream_t s, const Params &P, const StepArgs &a) {
 
 template <int MAXN, int NB, bool CODD, int FIX = kNoFix>
 void reset_one(dim3 grid, hipStream_t s, const Params &P, int64_t n, int8_t *board, uint64_t *rng, int32_t *timer,
-               uint64_t *eff, const uint8_t *env_mask, int mask_bits) {
+               uint64_t *eff, const uint8_t *env_mask, int mask_bits, int epw) {
     const size_t lds = sizeof(Ws<MAXN, false>);
     hipLaunchKernelGGL((reset_kernel<MAXN, NB, CODD, FIX>), grid, dim3(64), lds, s, P, n, board, rng, timer, eff,
-                       env_mask, mask_bits);
+                       env_mask, mask_bits, epw);
 }
 
 template <int MAXN>
@@ -101,14 +101,14 @@ void launch_step512(bool gen, dim3 grid, hipStream_t s, const Params &P, const S
 }
 
 void launch_reset512(dim3 grid, hipStream_t s, const Params &P, int64_t n, int8_t *board, uint64_t *rng,
-                     int32_t *timer, uint64_t *eff, const uint8_t *env_mask, int mask_bits) {
+                     int32_t *timer, uint64_t *eff, const uint8_t *env_mask, int mask_bits, int epw) {
     // NB = colour bit-planes of the row-plane generate (bp_generate)
-    if (is_shape<kFixReset20>(P)) { reset_one<512, 3, false, kFixReset20>(grid, s, P, n, board, rng, timer, eff, env_mask, mask_bits); return; }
+    if (is_shape<kFixReset20>(P)) { reset_one<512, 3, false, kFixReset20>(grid, s, P, n, board, rng, timer, eff, env_mask, mask_bits, epw); return; }
     switch (sb_planes(P.k)) {
-    case 1: reset_one<512, 1, false>(grid, s, P, n, board, rng, timer, eff, env_mask, mask_bits); break;
-    case 2: reset_one<512, 2, false>(grid, s, P, n, board, rng, timer, eff, env_mask, mask_bits); break;
-    case 3: reset_one<512, 3, false>(grid, s, P, n, board, rng, timer, eff, env_mask, mask_bits); break;
-    default: reset_one<512, 4, false>(grid, s, P, n, board, rng, timer, eff, env_mask, mask_bits); break;
+    case 1: reset_one<512, 1, false>(grid, s, P, n, board, rng, timer, eff, env_mask, mask_bits, epw); break;
+    case 2: reset_one<512, 2, false>(grid, s, P, n, board, rng, timer, eff, env_mask, mask_bits, epw); break;
+    case 3: reset_one<512, 3, false>(grid, s, P, n, board, rng, timer, eff, env_mask, mask_bits, epw); break;
+    default: reset_one<512, 4, false>(grid, s, P, n, board, rng, timer, eff, env_mask, mask_bits, epw); break;
     }
 }
 void launch_effective512(dim3 grid, hipStream_t s, const Params &P, int64_t n, const int8_t *board, uint64_t *eff) {
@@ -118,19 +118,19 @@ void launch_effective512(dim3 grid, hipStream_t s, const Params &P, int64_t n, c
 
 #if TMG_TU == 5
 void launch_reset128(bool sb, dim3 grid, hipStream_t s, const Params &P, int64_t n, int8_t *board, uint64_t *rng,
-                     int32_t *timer, uint64_t *eff, const uint8_t *env_mask, int mask_bits) {
-    if (!sb) { reset_one<128, 0, false>(grid, s, P, n, board, rng, timer, eff, env_mask, mask_bits); return; }
-    if (is_shape<kFixReset10>(P)) { reset_one<128, 2, false, kFixReset10>(grid, s, P, n, board, rng, timer, eff, env_mask, mask_bits); return; }
+                     int32_t *timer, uint64_t *eff, const uint8_t *env_mask, int mask_bits, int epw) {
+    if (!sb) { reset_one<128, 0, false>(grid, s, P, n, board, rng, timer, eff, env_mask, mask_bits, epw); return; }
+    if (is_shape<kFixReset10>(P)) { reset_one<128, 2, false, kFixReset10>(grid, s, P, n, board, rng, timer, eff, env_mask, mask_bits, epw); return; }
     const bool codd = P.C & 1;
     switch (sb_planes(P.k)) {
-    case 1: codd ? reset_one<128, 1, true>(grid, s, P, n, board, rng, timer, eff, env_mask, mask_bits)
-                 : reset_one<128, 1, false>(grid, s, P, n, board, rng, timer, eff, env_mask, mask_bits); break;
-    case 2: codd ? reset_one<128, 2, true>(grid, s, P, n, board, rng, timer, eff, env_mask, mask_bits)
-                 : reset_one<128, 2, false>(grid, s, P, n, board, rng, timer, eff, env_mask, mask_bits); break;
-    case 3: codd ? reset_one<128, 3, true>(grid, s, P, n, board, rng, timer, eff, env_mask, mask_bits)
-                 : reset_one<128, 3, false>(grid, s, P, n, board, rng, timer, eff, env_mask, mask_bits); break;
-    default: codd ? reset_one<128, 4, true>(grid, s, P, n, board, rng, timer, eff, env_mask, mask_bits)
-                  : reset_one<128, 4, false>(grid, s, P, n, board, rng, timer, eff, env_mask, mask_bits); break;
+    case 1: codd ? reset_one<128, 1, true>(grid, s, P, n, board, rng, timer, eff, env_mask, mask_bits, epw)
+                 : reset_one<128, 1, false>(grid, s, P, n, board, rng, timer, eff, env_mask, mask_bits, epw); break;
+    case 2: codd ? reset_one<128, 2, true>(grid, s, P, n, board, rng, timer, eff, env_mask, mask_bits, epw)
+                 : reset_one<128, 2, false>(grid, s, P, n, board, rng, timer, eff, env_mask, mask_bits, epw); break;
+    case 3: codd ? reset_one<128, 3, true>(grid, s, P, n, board, rng, timer, eff, env_mask, mask_bits, epw)
+                 : reset_one<128, 3, false>(grid, s, P, n, board, rng, timer, eff, env_mask, mask_bits, epw); break;
+    default: codd ? reset_one<128, 4, true>(grid, s, P, n, board, rng, timer, eff, env_mask, mask_bits, epw)
+                  : reset_one<128, 4, false>(grid, s, P, n, board, rng, timer, eff, env_mask, mask_bits, epw); break;
     }
 }
 void launch_effective128(dim3 grid, hipStream_t s, const Params &P, int64_t n, const int8_t *board, uint64_t *eff) {

@@ -39,11 +39,11 @@ void launch_step512(bool gen, dim3 grid, hipStream_t s, const Params &P, const S
 void launch_spill128(hipStream_t s, const Params &P, const StepArgs &a);
 void launch_spill512(hipStream_t s, const Params &P, const StepArgs &a);
 void launch_reset512(dim3 grid, hipStream_t s, const Params &P, int64_t n, int8_t *board, uint64_t *rng,
-                     int32_t *timer, uint64_t *eff, const uint8_t *env_mask, int mask_bits);
+                     int32_t *timer, uint64_t *eff, const uint8_t *env_mask, int mask_bits, int epw);
 void launch_effective512(dim3 grid, hipStream_t s, const Params &P, int64_t n, const int8_t *board, uint64_t *eff);
 // TU 5 — <= 128-cell reset / effective kernels
 void launch_reset128(bool sb, dim3 grid, hipStream_t s, const Params &P, int64_t n, int8_t *board, uint64_t *rng,
-                     int32_t *timer, uint64_t *eff, const uint8_t *env_mask, int mask_bits);
+                     int32_t *timer, uint64_t *eff, const uint8_t *env_mask, int mask_bits, int epw);
 void launch_effective128(dim3 grid, hipStream_t s, const Params &P, int64_t n, const int8_t *board, uint64_t *eff);
 // TU 6 — the callers either side (tmg_aux.hip)
 void launch_onehot(hipStream_t s, int64_t n, int N, int k, int nsel, int4 sel, const int8_t *board, void *out,

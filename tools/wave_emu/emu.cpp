@@ -275,7 +275,9 @@ static void emu_step_sb(EmuStep &S) {
 template <int MAXN, int NB, bool CODD, int FIX = tmg::kNoFix>
 static void emu_reset_kernel(const tmg::Params &P, int64_t n, int8_t *board, uint64_t *rng, int32_t *timer, uint64_t *eff,
                              const uint8_t *mask, int bits) {
-    run_blocks(n, sizeof(tmg::Ws<MAXN, false>), [&] { tmg::reset_kernel<MAXN, NB, CODD, FIX>(P, n, board, rng, timer, eff, mask, bits); });
+    const int epw = mask ? tmg::kMaskedResetEnvs : 1;                 // as tmg_capi.hip do_reset
+    run_blocks((n + epw - 1) / epw, sizeof(tmg::Ws<MAXN, false>),
+               [&] { tmg::reset_kernel<MAXN, NB, CODD, FIX>(P, n, board, rng, timer, eff, mask, bits, epw); });
 }
 template <bool CODD>
 static void emu_reset_sb(const tmg::Params &P, int64_t n, int8_t *board, uint64_t *rng, int32_t *timer, uint64_t *eff,
