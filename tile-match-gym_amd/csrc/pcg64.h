@@ -103,25 +103,10 @@ __host__ __device__ __forceinline__ U128 jump128(const U128 &A, const U128 &f, c
 #endif
 }
 
-#ifndef TMG_XSLAB
-#define TMG_XSLAB 1
-#endif
 __host__ __device__ __forceinline__ uint64_t xsl_rr(U128 s) {
-#if defined(__HIP_DEVICE_COMPILE__) && TMG_XSLAB
-    // 64-bit rotate as two funnel shifts of the halves (v_alignbit uses the
-    // shift's low 5 bits) and a swap when rot >= 32 (the state's top bit): all
-    // full-rate 32-bit ops, where the 64-bit shifts issue at the multiplies' rate
-    const uint32_t hh = (uint32_t)(s.hi >> 32);
-    const uint32_t xl = (uint32_t)s.hi ^ (uint32_t)s.lo, xh = hh ^ (uint32_t)(s.lo >> 32);
-    const uint32_t rot = hh >> 26;                         // state >> 122
-    const uint32_t a = __builtin_amdgcn_alignbit(xh, xl, rot), b = __builtin_amdgcn_alignbit(xl, xh, rot);
-    const bool sw = (int)hh < 0;
-    return ((uint64_t)(sw ? a : b) << 32) | (sw ? b : a);
-#else
     uint64_t x = s.hi ^ s.lo;
     unsigned rot = (unsigned)(s.hi >> 58);                 // state >> 122
     return (x >> rot) | (x << ((64u - rot) & 63u));
-#endif
 }
 
 // PCG_DEFAULT_MULTIPLIER_128

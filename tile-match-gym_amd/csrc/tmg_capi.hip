@@ -132,8 +132,8 @@ static int set_device(tmg_ctx *ctx) {
 static int do_reset(tmg_ctx *ctx, const Params &P, int64_t n, int8_t *board, uint64_t *rng, int32_t *timer,
                     uint64_t *eff, const uint8_t *env_mask, int mask_bits, hipStream_t s) {
     // a masked reset (the deferred autoreset after every general step; most
-    // find no finished env) takes tmg::kMaskedResetEnvs envs per wave
-    const int epw = env_mask ? tmg::kMaskedResetEnvs : 1;
+    // find no finished env) takes several envs per wave
+    const int epw = !env_mask ? 1 : ctx->maxn == 128 ? tmg::kMaskedResetEnvs128 : tmg::kMaskedResetEnvs512;
     const dim3 grid = tmg::env_grid((n + epw - 1) / epw);
     if (ctx->maxn == 128) tmg::launch_reset128(ctx->sb, grid, s, P, n, board, rng, timer, eff, env_mask, mask_bits, epw);
     else tmg::launch_reset512(grid, s, P, n, board, rng, timer, eff, env_mask, mask_bits, epw);

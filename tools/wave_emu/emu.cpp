@@ -275,7 +275,7 @@ static void emu_step_sb(EmuStep &S) {
 template <int MAXN, int NB, bool CODD, int FIX = tmg::kNoFix>
 static void emu_reset_kernel(const tmg::Params &P, int64_t n, int8_t *board, uint64_t *rng, int32_t *timer, uint64_t *eff,
                              const uint8_t *mask, int bits) {
-    const int epw = mask ? tmg::kMaskedResetEnvs : 1;                 // as tmg_capi.hip do_reset
+    const int epw = !mask ? 1 : MAXN == 128 ? tmg::kMaskedResetEnvs128 : tmg::kMaskedResetEnvs512;   // as do_reset
     run_blocks((n + epw - 1) / epw, sizeof(tmg::Ws<MAXN, false>),
                [&] { tmg::reset_kernel<MAXN, NB, CODD, FIX>(P, n, board, rng, timer, eff, mask, bits, epw); });
 }
