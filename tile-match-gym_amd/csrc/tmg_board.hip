@@ -31,21 +31,15 @@ namespace tmg {
 // Minimum waves per SIMD asked of the register allocator (launch bounds), per
 // kernel; each measured on the MI355X against its neighbours.
 constexpr int kLean128Waves = 7;     // step_kernel<128, false>: the c2 / c4 kernel (72 VGPRs)
-constexpr int kGen128Waves = 5;      // step_kernel<128, true>: c3 (96 VGPRs; 6 / 7 spill and lose)
+constexpr int kGen128Waves = 5;      // step_kernel<128, true>: c3 (96 VGPRs; 6 / 7 spill and lose, also specialised)
 constexpr int kReset512Waves = 7;    // reset_kernel<512>: c5's regeneration
 constexpr int kReset128Waves = 8;    // reset_kernel<128> specialised for 10x10 k4 (c3): 63 VGPRs
-#ifndef TMG_MRE128
-#define TMG_MRE128 8
-#endif
-#ifndef TMG_MRE512
-#define TMG_MRE512 2
-#endif
-#ifndef TMG_G6
-#define TMG_G6 0
-#endif
-// envs per wave of a masked reset_kernel launch (the deferred autoreset)
-constexpr int kMaskedResetEnvs128 = TMG_MRE128;
-constexpr int kMaskedResetEnvs512 = TMG_MRE512;
+// envs per wave of a masked reset_kernel launch (the deferred autoreset after a
+// general step; 29 of 30 find no finished env).  10x10 boards: 1 / 2 / 4 / 8 /
+// 16 measured c3 6.97 / 7.10 / 7.19 / 7.17 / 7.15 x 10^8; 20x20 boards, whose
+// regenerations are long: 2 (4 made the storm 4 % slower).
+constexpr int kMaskedResetEnvs128 = 8;
+constexpr int kMaskedResetEnvs512 = 2;
 constexpr int kC5StepWaves = 4;      // step_kernel<512, true> specialised for c5 (128 VGPRs; 3 measured the same)
 
 // compiler-only ordering point between a wave's LDS loads and later stores
@@ -2336,7 +2330,7 @@ __device__ __forceinline__ void assume_shape(const Params &P) {
 }
 
 template <int MAXN, bool GEN, int SBNB = 0, bool CODD = false, int FIX = kNoFix>
-__global__ __launch_bounds__(64, MAXN == 128 ? (GEN ? (TMG_G6 && FIX != kNoFix ? 6 : kGen128Waves) : kLean128Waves) : (FIX == kFixC5 ? kC5StepWaves : 1)) void step_kernel(
+__global__ __launch_bounds__(64, MAXN == 128 ? (GEN ? kGen128Waves : kLean128Waves) : (FIX == kFixC5 ? kC5StepWaves : 1)) void step_kernel(
     Params P_, int64_t n, int8_t *__restrict__ board, uint64_t *__restrict__ rng, int32_t *__restrict__ timer,
     const int32_t *__restrict__ actions, int32_t *__restrict__ reward, int32_t *__restrict__ n_new,
     int32_t *__restrict__ n_act, uint8_t *__restrict__ flags_out, uint64_t *__restrict__ eff, int trust_eff,

@@ -114,6 +114,8 @@ K32(k_bfe, "v_bfe_u32 %0, %0, %1, 1")
 K32(k_dpp, "v_mov_b32_dpp %0, %0 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf")
 K32(k_cndmask, "v_cndmask_b32 %0, %0, %1, vcc")
 K32(k_xor, "v_xor_b32 %0, %0, %1")
+K32(k_add_e64, "v_add_u32_e64 %0, %0, %1")               // the same add in the 8-byte VOP3 encoding
+K32(k_or3, "v_or3_b32 %0, %0, %1, %1")
 
 #define K64(NAME, ASM)                                                                  \
     __global__ void NAME(uint32_t *out, uint32_t seed) {                                \
@@ -143,7 +145,7 @@ int main() {
     K ks[] = {{"v_add_u32", k_add}, {"v_mul_lo_u32", k_mul_lo}, {"v_mul_hi_u32", k_mul_hi},
               {"v_mul_u32_u24", k_mul_u24}, {"v_mad_u64_u32", k_mad64}, {"v_lshl_add_u64", k_lshl_add64},
               {"v_alignbit_b32", k_alignbit}, {"v_bfe_u32", k_bfe}, {"v_mov_b32_dpp", k_dpp},
-              {"v_cndmask_b32", k_cndmask}, {"v_xor_b32", k_xor}, {"v_lshlrev_b64", k_lshl64},
+              {"v_cndmask_b32", k_cndmask}, {"v_xor_b32", k_xor}, {"v_add_u32_e64", k_add_e64}, {"v_or3_b32", k_or3}, {"v_lshlrev_b64", k_lshl64},
               {"v_mov_b64", k_mov64}};
     hipEvent_t a, b;
     hipEventCreate(&a);
