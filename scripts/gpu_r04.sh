@@ -106,6 +106,16 @@ pmcmb)
   done
   done
   ;;
+window)
+  # the driver's short window (--steps 20 --warmup 5) against longer ones, and its kernel timeline
+  for k in 20 40 80; do
+    timeout -k 10 200 python bench.py --steps $k --warmup 5 --no-cpu-baseline > $OUT/c2_window_$k.log 2>&1 || exit 1
+    echo "steps $k: $(tail -1 $OUT/c2_window_$k.log | cut -c88-140)"
+  done
+  timeout -k 10 200 rocprofv3 --kernel-trace -d $OUT/window_trace -o run --output-format csv -- \
+    python3 bench.py --steps 20 --warmup 5 --no-cpu-baseline > $OUT/window_trace.log 2>&1 || { echo "trace failed"; tail -5 $OUT/window_trace.log; exit 1; }
+  python3 tools/window_trace.py $OUT/window_trace 20 3 | tee $OUT/window_trace.txt
+  ;;
 all)
   STAGE=tests bash scripts/gpu_r04.sh && STAGE=deep bash scripts/gpu_r04.sh && STAGE=bench bash scripts/gpu_r04.sh
   ;;
