@@ -112,6 +112,13 @@ window)
     timeout -k 10 200 python bench.py --steps $k --warmup 5 --no-cpu-baseline > $OUT/c2_window_$k.log 2>&1 || exit 1
     echo "steps $k: $(tail -1 $OUT/c2_window_$k.log | cut -c88-140)"
   done
+  for v in "--phase-interleave" "--phase-align 0"; do
+    for k in 20 300; do
+      n=$(echo "$v" | tr -d ' -')_$k
+      timeout -k 10 200 python bench.py --steps $k --warmup 5 --no-cpu-baseline $v > $OUT/c2_window_$n.log 2>&1 || exit 1
+      echo "$v steps $k: $(tail -1 $OUT/c2_window_$n.log | cut -c88-140)"
+    done
+  done
   timeout -k 10 200 rocprofv3 --kernel-trace -d $OUT/window_trace -o run --output-format csv -- \
     python3 bench.py --steps 20 --warmup 5 --no-cpu-baseline > $OUT/window_trace.log 2>&1 || { echo "trace failed"; tail -5 $OUT/window_trace.log; exit 1; }
   python3 tools/window_trace.py $OUT/window_trace 20 3 | tee $OUT/window_trace.txt
