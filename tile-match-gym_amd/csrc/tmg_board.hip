@@ -44,6 +44,15 @@ constexpr int kC5StepWaves = 4;      // step_kernel<512, true> specialised for c
 
 // compiler-only ordering point between a wave's LDS loads and later stores
 #define WFENCE() __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront")
+#ifndef TMG_TAKE1
+#define TMG_TAKE1 1
+#endif
+// an empty asm reading eight VGPR values: all of them are loaded (and their
+// loads issued) before anything after it
+#ifndef TMG_KEEP_V8
+#define TMG_KEEP_V8(a, b, c, d, e, f, g, h) \
+    asm volatile("" ::"v"(a), "v"(b), "v"(c), "v"(d), "v"(e), "v"(f), "v"(g), "v"(h))
+#endif
 
 // dynamic LDS of the workgroup (overridable only by the host-side wave
 // emulator in tools/wave_emu, which runs this file under AddressSanitizer)
@@ -1153,22 +1162,52 @@ __device__ __forceinline__ void bp_ring_state(const BpJump &J, WS &w, const BpRi
 }
 
 // rows 0..row <- the ring's next (row + 1) * C colours (colour plane only)
-template <int NB, class WS>
+// AHEAD: the next redraw's batch is filled (when fewer than 128 colours would
+// be left) between issuing the ring reads and using them, under their latency
+template <int NB, bool AHEAD = false, class WS>
 __device__ __forceinline__ void bp_take(const Params &P, WS &w, int lane, const BpJump &J, BpRing &r, int row,
                                         uint32_t cm, RowPlanes<NB> &pl) {
     const int M = (row + 1) * P.C;
     while (r.fill - r.cons < M) bp_ring_fill<NB>(P, w, lane, J, r);
-    WSYNC();
+#if TMG_TAKE1
+    // One wave per workgroup, and a wave's LDS instructions execute in order:
+    // the reads below see lane 0's ring stores (bp_ring_fill) without waiting
+    // for those stores to complete, so a compiler-only fence, not WSYNC's wait
+    WFENCE();
     const uint32_t *ring = bp_ring(w);
     const int o = r.cons + lane * P.C;                           // this lane's row starts here
     const int d = (o >> 5) & (kBpRingDw - 1);
     const uint32_t s = (uint32_t)o & 31u;
     const uint32_t in = lane <= row ? cm : 0u;                   // the cells this take rewrites
+    uint32_t lo[NB], hi[NB];                                     // every plane's reads issued together:
+#pragma unroll                                                   // one LDS round trip per take (the
+    for (int b = 0; b < NB; b++) {                               // scheduler otherwise waits for plane 0
+        lo[b] = ring[b * kBpPlaneDw + d];                        // before issuing the others)
+        hi[b] = ring[b * kBpPlaneDw + d + 1];
+    }
+    if constexpr (AHEAD) {
+        if (r.fill - r.cons - M < 128) bp_ring_fill<NB>(P, w, lane, J, r);
+    }
+    TMG_KEEP_V8(lo[0], hi[0], lo[NB > 1 ? 1 : 0], hi[NB > 1 ? 1 : 0], lo[NB > 2 ? 2 : 0], hi[NB > 2 ? 2 : 0],
+                lo[NB > 3 ? 3 : 0], hi[NB > 3 ? 3 : 0]);
+#pragma unroll
+    for (int b = 0; b < NB; b++) {
+        const uint32_t v = __builtin_amdgcn_alignbit(hi[b], lo[b], s);
+        pl.p[b] = (v & in) | (pl.p[b] & ~in);
+    }
+#else
+    WSYNC();
+    const uint32_t *ring = bp_ring(w);
+    const int o = r.cons + lane * P.C;
+    const int d = (o >> 5) & (kBpRingDw - 1);
+    const uint32_t s = (uint32_t)o & 31u;
+    const uint32_t in = lane <= row ? cm : 0u;
 #pragma unroll
     for (int b = 0; b < NB; b++) {
         const uint32_t v = __builtin_amdgcn_alignbit(ring[b * kBpPlaneDw + d + 1], ring[b * kBpPlaneDw + d], s);
         pl.p[b] = (v & in) | (pl.p[b] & ~in);
     }
+#endif
     r.cons += M;
 }
 
@@ -1255,10 +1294,12 @@ __device__ __forceinline__ int bp_generate(const Params &P, WS &w, int lane, Rng
     int fl = 0;
     for (int shuffles = 0;; shuffles++) {
         for (;;) {                                                       // remove_colour_lines, :120-131
+#if !TMG_TAKE1
             if (r.fill - r.cons < 128) bp_ring_fill<NB>(P, w, lane, J, r);   // the next redraw's colours, beside the search
+#endif
             const int r0 = bp_first_line_row<NB>(pl, hml, vml);
             if (r0 < 0) break;
-            bp_take<NB>(P, w, lane, J, r, R - 1 < r0 + 1 ? R - 1 : r0 + 1, cm, pl);   // rows 0..min(R-1, r0+1)
+            bp_take<NB, TMG_TAKE1 != 0>(P, w, lane, J, r, R - 1 < r0 + 1 ? R - 1 : r0 + 1, cm, pl);   // rows 0..min(R-1, r0+1)
             if (r.rej) break;
         }
         if (r.rej) break;

@@ -26,7 +26,7 @@ def main():
             if "tmg::" not in n:
                 continue
             q = r.get("Stream_Id") or r.get("Queue_Id")
-            rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), q, n.split("<")[0].replace("tmg::", "")))
+            rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), q, n.split("<")[0].replace("void ", "").replace("tmg::", "").strip()))
     rows.sort()
     steps = [i for i, r in enumerate(rows) if r[3] == "step_kernel"]
     first = steps[-K * G]
