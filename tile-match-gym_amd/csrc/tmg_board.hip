@@ -1168,6 +1168,8 @@ template <int NB, bool AHEAD = false, class WS>
 __device__ __forceinline__ void bp_take(const Params &P, WS &w, int lane, const BpJump &J, BpRing &r, int row,
                                         uint32_t cm, RowPlanes<NB> &pl) {
     const int M = (row + 1) * P.C;
+    r.fill = __builtin_amdgcn_readfirstlane(r.fill);             // wave-uniform (see bp_generate)
+    r.cons = __builtin_amdgcn_readfirstlane(r.cons);
     while (r.fill - r.cons < M) bp_ring_fill<NB>(P, w, lane, J, r);
 #if TMG_TAKE1
     // One wave per workgroup, and a wave's LDS instructions execute in order:
@@ -1279,6 +1281,10 @@ __device__ __forceinline__ RowPlanes<NB> bp_from_lds(const Params &P, const WS &
 template <int NB, class WS>
 __device__ __forceinline__ int bp_generate(const Params &P, WS &w, int lane, Rng &g) {
     const int R = P.R, C = P.C, N = P.N;
+    // g is wave-uniform; said so explicitly, since where the divergence analysis
+    // cannot see it (the lean step kernel's inline autoreset) the ring's
+    // counters and state otherwise go to VGPRs and its loops run exec-masked
+    rng_bcast(g);
     const Rng g0 = g;
     const BpJump J = load_bp_jump(P, lane, g);
     const uint32_t cm = C >= 32 ? ~0u : (1u << C) - 1u;
