@@ -2,8 +2,12 @@
 # Round-4 GPU evidence.  Usage (through gpurun, from the repo root):
 #   STAGE=tests bash scripts/gpu_r04.sh   # pytest -m gpu (all but the deep rollouts), smoke, c2 bench
 #   STAGE=deep  bash scripts/gpu_r04.sh   # the deep rollouts vs the oracle + the TMG_COVER branch counts
-#   STAGE=bench bash scripts/gpu_r04.sh   # c2 / c3 / c5 bench lines with the CPU baseline + driver window
-#   STAGE=prof  bash scripts/gpu_r04.sh   # rocprofv3 --kernel-trace --stats of the c2 / c3 / c5 benches
+#   STAGE=bench bash scripts/gpu_r04.sh   # c2 / c3 / c5 / c4-shard bench lines with the CPU baseline + driver window
+#   STAGE=prof  bash scripts/gpu_r04.sh   # rocprofv3 --kernel-trace --stats of the c2 / c3 / c5 / c4 benches
+#   STAGE=abx   bash scripts/gpu_r04.sh   # A/B: product vs _lib/libtmg_ab_<name>.so for AB="name ..." (scripts/build_ab.sh)
+#   STAGE=pmcmb bash scripts/gpu_r04.sh   # SQ instruction counts per launch kind (tools/microbench.py, tools/pmc_micro.py)
+#   STAGE=window bash scripts/gpu_r04.sh  # the driver's 20-step window vs longer ones + its kernel timeline
+#   STAGE=final bash scripts/gpu_r04.sh   # deep, bench, pmcmb (c2 c5), facade probe
 #   STAGE=all   bash scripts/gpu_r04.sh   # tests, deep, bench
 # Each GPU step has its own time limit; the script stops at the first failure.
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
@@ -122,6 +126,13 @@ window)
   timeout -k 10 200 rocprofv3 --kernel-trace -d $OUT/window_trace -o run --output-format csv -- \
     python3 bench.py --steps 20 --warmup 5 --no-cpu-baseline > $OUT/window_trace.log 2>&1 || { echo "trace failed"; tail -5 $OUT/window_trace.log; exit 1; }
   python3 tools/window_trace.py $OUT/window_trace 20 3 | tee $OUT/window_trace.txt
+  ;;
+final)
+  # round-end evidence: deep rollouts + cover counts, bench lines with CPU baselines (c2 c3 c5 and the c4
+  # shard) + the driver's window, SQ counts per launch kind (c2, c5), the single-env facade probe
+  STAGE=deep bash scripts/gpu_r04.sh && STAGE=bench bash scripts/gpu_r04.sh || exit 1
+  STAGE=pmcmb CONFIGS="c2 c5" bash scripts/gpu_r04.sh || exit 1
+  timeout -k 10 120 python tools/facade_probe.py > $OUT/facade_probe.log 2>&1 && cat $OUT/facade_probe.log
   ;;
 all)
   STAGE=tests bash scripts/gpu_r04.sh && STAGE=deep bash scripts/gpu_r04.sh && STAGE=bench bash scripts/gpu_r04.sh
