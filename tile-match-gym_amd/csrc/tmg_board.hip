@@ -47,6 +47,9 @@ constexpr int kC5StepWaves = 4;      // step_kernel<512, true> specialised for c
 #ifndef TMG_TAKE1
 #define TMG_TAKE1 1
 #endif
+#ifndef TMG_PF
+#define TMG_PF 1
+#endif
 // an empty asm reading eight VGPR values: all of them are loaded (and their
 // loads issued) before anything after it
 #ifndef TMG_KEEP_V8
@@ -2225,7 +2228,26 @@ __device__ __forceinline__ uint32_t step_env(
     action_coords(P.R, P.C, a, r1, c1, r2, c2);
     const int p1 = r1 * P.C + c1, p2 = r2 * P.C + c2;
 
+#if TMG_PF
+    // The effective path's loads issued together, before anything waits on
+    // one: the board (when whole dwords), the RNG state and this lane's
+    // jump-table row.  One memory round trip instead of three dependent ones
+    // (board -> LDS -> precondition -> RNG -> jump table).
+    const int nbw = (2 * N) >> 2;
+    const bool bwhole = ((2 * N) & 3) == 0 && nbw <= 64;
+    const uint32_t bw = bwhole ? reinterpret_cast<const uint32_t *>(gb)[lane < nbw ? lane : 0] : 0u;
+    const uint64_t *rp = rng + e * 5;
+    const uint64_t q0 = rp[0], q1 = rp[1], q2 = rp[2], q3 = rp[3], q4 = rp[4];
+    const uint64_t *jt = P.jump + lane * 4;
+    const uint64_t j0 = jt[0], j1 = jt[1], j2 = jt[2], j3 = jt[3];
+    if (bwhole) {
+        if (lane < nbw) reinterpret_cast<uint32_t *>(w.brd)[lane] = bw;
+    } else {
+        load_board(P, w, lane, gb);
+    }
+#else
     load_board(P, w, lane, gb);
+#endif
     if constexpr (GEN) {
         for (int p = lane; p < N; p += 64) w.mark[p] = 0;
     }
@@ -2243,8 +2265,17 @@ __device__ __forceinline__ uint32_t step_env(
         bool ex = lane == 0 ? eff_exact(P, w.brd, a) : false;
         effective = __ballot(ex) != 0ULL;
     }
+#if TMG_PF
+    Rng g;
+    g.slo = bcast64(q0); g.shi = bcast64(q1); g.ilo = bcast64(q2); g.ihi = bcast64(q3); g.h = bcast64(q4);
+    LaneJump J;
+    J.Aj = U128{j0, j1};
+    J.Gj = U128{j2, j3};
+    J.incG = mul128(U128{g.ilo, g.ihi}, J.Gj);
+#else
     Rng g = load_rng(rng + e * 5);
     const LaneJump J = load_jump(P, lane, g);
+#endif
     const Cells<MAXN / 64> cl = make_cells<MAXN / 64>(P, lane);
     int elim = 0, nn = 0, na = 0;
     bool changed = false;
