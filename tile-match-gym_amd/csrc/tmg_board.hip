@@ -44,12 +44,6 @@ constexpr int kC5StepWaves = 4;      // step_kernel<512, true> specialised for c
 
 // compiler-only ordering point between a wave's LDS loads and later stores
 #define WFENCE() __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront")
-#ifndef TMG_TAKE1
-#define TMG_TAKE1 1
-#endif
-#ifndef TMG_PF
-#define TMG_PF 1
-#endif
 // an empty asm reading eight VGPR values: all of them are loaded (and their
 // loads issued) before anything after it
 #ifndef TMG_KEEP_V8
@@ -1174,7 +1168,6 @@ __device__ __forceinline__ void bp_take(const Params &P, WS &w, int lane, const 
     r.fill = __builtin_amdgcn_readfirstlane(r.fill);             // wave-uniform (see bp_generate)
     r.cons = __builtin_amdgcn_readfirstlane(r.cons);
     while (r.fill - r.cons < M) bp_ring_fill<NB>(P, w, lane, J, r);
-#if TMG_TAKE1
     // One wave per workgroup, and a wave's LDS instructions execute in order:
     // the reads below see lane 0's ring stores (bp_ring_fill) without waiting
     // for those stores to complete, so a compiler-only fence, not WSYNC's wait
@@ -1200,19 +1193,6 @@ __device__ __forceinline__ void bp_take(const Params &P, WS &w, int lane, const 
         const uint32_t v = __builtin_amdgcn_alignbit(hi[b], lo[b], s);
         pl.p[b] = (v & in) | (pl.p[b] & ~in);
     }
-#else
-    WSYNC();
-    const uint32_t *ring = bp_ring(w);
-    const int o = r.cons + lane * P.C;
-    const int d = (o >> 5) & (kBpRingDw - 1);
-    const uint32_t s = (uint32_t)o & 31u;
-    const uint32_t in = lane <= row ? cm : 0u;
-#pragma unroll
-    for (int b = 0; b < NB; b++) {
-        const uint32_t v = __builtin_amdgcn_alignbit(ring[b * kBpPlaneDw + d + 1], ring[b * kBpPlaneDw + d], s);
-        pl.p[b] = (v & in) | (pl.p[b] & ~in);
-    }
-#endif
     r.cons += M;
 }
 
@@ -1303,12 +1283,9 @@ __device__ __forceinline__ int bp_generate(const Params &P, WS &w, int lane, Rng
     int fl = 0;
     for (int shuffles = 0;; shuffles++) {
         for (;;) {                                                       // remove_colour_lines, :120-131
-#if !TMG_TAKE1
-            if (r.fill - r.cons < 128) bp_ring_fill<NB>(P, w, lane, J, r);   // the next redraw's colours, beside the search
-#endif
             const int r0 = bp_first_line_row<NB>(pl, hml, vml);
             if (r0 < 0) break;
-            bp_take<NB, TMG_TAKE1 != 0>(P, w, lane, J, r, R - 1 < r0 + 1 ? R - 1 : r0 + 1, cm, pl);   // rows 0..min(R-1, r0+1)
+            bp_take<NB, true>(P, w, lane, J, r, R - 1 < r0 + 1 ? R - 1 : r0 + 1, cm, pl);   // rows 0..min(R-1, r0+1)
             if (r.rej) break;
         }
         if (r.rej) break;
@@ -2228,7 +2205,6 @@ __device__ __forceinline__ uint32_t step_env(
     action_coords(P.R, P.C, a, r1, c1, r2, c2);
     const int p1 = r1 * P.C + c1, p2 = r2 * P.C + c2;
 
-#if TMG_PF
     // The effective path's loads issued together, before anything waits on
     // one: the board (when whole dwords), the RNG state and this lane's
     // jump-table row.  One memory round trip instead of three dependent ones
@@ -2245,9 +2221,6 @@ __device__ __forceinline__ uint32_t step_env(
     } else {
         load_board(P, w, lane, gb);
     }
-#else
-    load_board(P, w, lane, gb);
-#endif
     if constexpr (GEN) {
         for (int p = lane; p < N; p += 64) w.mark[p] = 0;
     }
@@ -2265,17 +2238,12 @@ __device__ __forceinline__ uint32_t step_env(
         bool ex = lane == 0 ? eff_exact(P, w.brd, a) : false;
         effective = __ballot(ex) != 0ULL;
     }
-#if TMG_PF
     Rng g;
     g.slo = bcast64(q0); g.shi = bcast64(q1); g.ilo = bcast64(q2); g.ihi = bcast64(q3); g.h = bcast64(q4);
     LaneJump J;
     J.Aj = U128{j0, j1};
     J.Gj = U128{j2, j3};
     J.incG = mul128(U128{g.ilo, g.ihi}, J.Gj);
-#else
-    Rng g = load_rng(rng + e * 5);
-    const LaneJump J = load_jump(P, lane, g);
-#endif
     const Cells<MAXN / 64> cl = make_cells<MAXN / 64>(P, lane);
     int elim = 0, nn = 0, na = 0;
     bool changed = false;
