@@ -132,3 +132,41 @@ def test_rare_paths_taken(name):
     missing = {s: counts[s] for s in VARIANTS[name][6] if counts[s] == 0}
     assert not missing, f"{name}: sites never taken: {missing} (counts {counts})"
     env.close()
+
+
+# (R, C, k, smask): the lean 128-cell reset, the 10x10 k4 reset specialised for c3, the c5 reset
+MASKED = [(5, 6, 7, 0), (10, 10, 4, 14), (20, 20, 6, 15)]
+
+
+@pytest.mark.parametrize("shape", MASKED)
+def test_masked_reset_subsets_vs_oracle(shape):
+    """reset(env_mask=...) (tile_match_env.py:84-91 for the selected envs only):
+    a masked reset_kernel launch takes several envs per wave (kMaskedResetEnvs*);
+    random subsets, whole groups and a ragged tail (n not a multiple of 8) all
+    regenerate exactly the selected boards, and leave every other env as it was."""
+    from tile_match_gym_amd.vec_env import TileMatchVecEnv
+    R, C, k, sm = shape
+    n = 1003
+    cl, co = specials(sm)
+    env = TileMatchVecEnv(n, R, C, k, 30, cl, co, seeds=range(7000, 7000 + n), device=DEV)
+    env.reset()
+    for t in range(3):                                    # move the streams on, differently per env
+        env.step_effective(t, key=KEY)
+    env.join()
+    rs = np.random.default_rng(sum(shape))
+    mask = rs.random(n) < 0.3
+    mask[8:16] = True                                     # one whole group of envs
+    mask[16:24] = False
+    mask[-3:] = True                                      # the ragged tail
+    before = {f: _host(env, f).copy() for f in ("board", "rng", "timer", "eff")}
+    o = orc.OracleBatch(R, C, k, sm, 30, env.rng_words().copy(), threads=16)
+    o.reset()                                             # every env regenerated from its own stream
+    env.reset(env_mask=torch.from_numpy(mask))
+    env.join()
+    for f in ("board", "rng", "timer", "eff"):
+        got = _host(env, f).reshape(n, -1)
+        want = np.where(mask[:, None], getattr(o, f).reshape(n, -1), before[f].reshape(n, -1))
+        bad = np.nonzero((got != want).any(axis=1))[0]
+        assert bad.size == 0, f"{shape}: {f} differs in {bad.size} envs, first {bad[:5]}"
+    assert env.status() == 0
+    env.close()
