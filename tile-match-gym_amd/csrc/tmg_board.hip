@@ -32,10 +32,7 @@ namespace tmg {
 // kernel; each measured on the MI355X against its neighbours.
 constexpr int kLean128Waves = 7;     // step_kernel<128, false>: the c2 / c4 kernel (72 VGPRs)
 constexpr int kGen128Waves = 5;      // step_kernel<128, true>: c3 (96 VGPRs; 6 / 7 spill and lose, also specialised)
-#ifndef TMG_R512W
-#define TMG_R512W 7
-#endif
-constexpr int kReset512Waves = TMG_R512W;    // reset_kernel<512>: c5's regeneration
+constexpr int kReset512Waves = 8;    // reset_kernel<512>: c5's regeneration (7: 0.8 % slower, profiles/r04/s7)
 constexpr int kReset128Waves = 8;    // reset_kernel<128> specialised for 10x10 k4 (c3): 63 VGPRs
 // envs per wave of a masked reset_kernel launch (the deferred autoreset after a
 // general step; 29 of 30 find no finished env).  10x10 boards: 1 / 2 / 4 / 8 /
