@@ -339,7 +339,6 @@ __device__ __forceinline__ int wave_max(int v) {
     return __builtin_amdgcn_readlane(v, 63);
 }
 
-__device__ __forceinline__ uint64_t lanemask_lt(int lane) { return lane ? (~0ULL >> (64 - lane)) : 0ULL; }
 // popcount of the bits of m below this lane (v_mbcnt: no lane mask kept in registers)
 __device__ __forceinline__ int popc_below(uint64_t m) {
     return (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
