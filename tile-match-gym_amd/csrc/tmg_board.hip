@@ -46,9 +46,6 @@ constexpr int kC5StepWaves = 4;      // step_kernel<512, true> specialised for c
 #define WFENCE() __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront")
 // an empty asm reading eight VGPR values: all of them are loaded (and their
 // loads issued) before anything after it
-#ifndef TMG_ONEBASE
-#define TMG_ONEBASE 1
-#endif
 #ifndef TMG_KEEP_V8
 #define TMG_KEEP_V8(a, b, c, d, e, f, g, h) \
     asm volatile("" ::"v"(a), "v"(b), "v"(c), "v"(d), "v"(e), "v"(f), "v"(g), "v"(h))
@@ -1099,12 +1096,12 @@ __device__ __forceinline__ void bp_ring_fill(const Params &P, WS &w, int lane, c
         }
     }
     const int q = (r.fill >> 5) & (kBpRingDw - 1);
-    if constexpr (WS::NP > 2 || TMG_ONEBASE) {
+    if constexpr (WS::NP > 2) {
         // 512-cell kernels: one VGPR base (ring + q) for every store.  The
         // planes, their guard copies and the batch's state slot (bp_slots +
         // 4 * (fill >> 7 & 7) = ring + 144 + q) sit at immediate offsets from
-        // it, where separate scalar bases each needed a v_mov.  (In the 128-cell
-        // lean kernel's inline autoreset this form costs a VGPR, and a wave.)
+        // it, where separate scalar bases each needed a v_mov.  (The 128-cell
+        // kernels measured the same either way, profiles/r04/s8.)
         uint32_t *ws = reinterpret_cast<uint32_t *>(&w);
         int at = (int)(bp_ring(w) - ws) + q;                         // dword index of ring + q (scalar)
         TMG_OPAQUE_V(at);
