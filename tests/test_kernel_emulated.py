@@ -201,3 +201,36 @@ def test_rare_paths_emulated(emu_lib, name):
     hits = dict(zip(COVER_NAMES, emu.cover(L, True)))
     missing = [s for s in sites if s != "shuffle_gen" and hits[s] == 0]
     assert not missing, (name, {s: int(hits[s]) for s in sites})
+
+
+@pytest.mark.parametrize("cfg", [(10, 10, 4, 0), (10, 10, 4, 14), (6, 6, 7, 14), (20, 20, 6, 15)])
+def test_masked_reset_subsets_emulated(emu_lib, cfg):
+    """reset(env_mask): the masked reset_kernel launch takes several envs per wave
+    (kMaskedResetEnvs*); a random subset, a whole group of envs and a ragged tail
+    regenerate exactly the selected boards (vs the oracle's reset of the same
+    streams) and leave the others untouched."""
+    from oracle import oracle as orc
+    from tile_match_gym_amd.seeding import batch_rng_words
+    emu, L = emu_lib
+    R, C, k, sm = cfg
+    n = 27 if R * C <= 128 else 11
+    w = batch_rng_words(range(3000, 3000 + n))
+    e = emu.EmuBatch(L, R, C, k, sm, 30, w)
+    e.reset()
+    rs = np.random.default_rng(R + C + k + sm)
+    A = 2 * R * C - R - C
+    for _ in range(2):                                      # move the streams on
+        e.step(rs.integers(0, A, n).astype(np.int32), True)
+    mask = (rs.random(n) < 0.4).astype(np.uint8)
+    if n > 16:
+        mask[:8] = 1                                        # a whole group of envs
+    mask[-1] = 1                                            # the ragged tail
+    before = {f: getattr(e, f).copy() for f in ("board", "rng", "timer", "eff")}
+    o = orc.OracleBatch(R, C, k, sm, 30, e.rng.copy())
+    o.reset()
+    e.reset(mask)
+    sel = mask.astype(bool)
+    for f in ("board", "rng", "timer", "eff"):
+        got = getattr(e, f).reshape(n, -1)
+        want = np.where(sel[:, None], getattr(o, f).reshape(n, -1), before[f].reshape(n, -1))
+        assert np.array_equal(got, want), f"{cfg}: {f}"

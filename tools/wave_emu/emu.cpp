@@ -368,6 +368,15 @@ int emu_reset(int R, int C, int k, int smask, int moves, int64_t n, int8_t *boar
     return 0;
 }
 
+// reset(env_mask): the masked reset_kernel launch (several envs per wave, as tmg_capi.hip do_reset)
+int emu_reset_masked(int R, int C, int k, int smask, int moves, int64_t n, int8_t *board, uint64_t *rng,
+                     int32_t *timer, uint64_t *eff, const uint8_t *mask, int bits) {
+    if (!g_jump_init) { tmg::build_jump_table(g_jump); g_jump_init = true; }
+    tmg::Params P = make_params(R, C, k, smask, moves, g_jump);
+    emu_do_reset(P, n, board, rng, timer, eff, mask, bits);
+    return 0;
+}
+
 int emu_effective(int R, int C, int k, int smask, int64_t n, const int8_t *board, uint64_t *eff) {
     if (!g_jump_init) { tmg::build_jump_table(g_jump); g_jump_init = true; }
     tmg::Params P = make_params(R, C, k, smask, 1, g_jump);

@@ -20,6 +20,7 @@ def load(asan=False):
     L = ctypes.CDLL(os.path.join(HERE, "libwave_emu_asan.so" if asan else os.environ.get("EMU_LIB", "libwave_emu.so")))
     L.emu_step.argtypes = [I, I, I, I, I, I64, P, P, P, P, P, P, P, P, P, I, I]
     L.emu_reset.argtypes = [I, I, I, I, I, I64, P, P, P, P]
+    L.emu_reset_masked.argtypes = [I, I, I, I, I, I64, P, P, P, P, P, I]
     L.emu_effective.argtypes = [I, I, I, I, I64, P, P]
     L.emu_spills.restype = ctypes.c_ulonglong
     L.emu_status.restype = ctypes.c_uint
@@ -54,9 +55,16 @@ class EmuBatch:
         self.flags = np.zeros(self.n, np.uint8)
         self.trust = False
 
-    def reset(self):
-        self.L.emu_reset(self.R, self.C, self.k, self.smask, self.num_moves, self.n, self.board.ctypes.data,
-                         self.rng.ctypes.data, self.timer.ctypes.data, self.eff.ctypes.data)
+    def reset(self, mask=None):
+        """reset(); with a uint8 mask, only the envs whose mask byte is non-zero (reset(env_mask=...))."""
+        if mask is None:
+            self.L.emu_reset(self.R, self.C, self.k, self.smask, self.num_moves, self.n, self.board.ctypes.data,
+                             self.rng.ctypes.data, self.timer.ctypes.data, self.eff.ctypes.data)
+        else:
+            m = np.ascontiguousarray(mask, dtype=np.uint8)
+            self.L.emu_reset_masked(self.R, self.C, self.k, self.smask, self.num_moves, self.n,
+                                    self.board.ctypes.data, self.rng.ctypes.data, self.timer.ctypes.data,
+                                    self.eff.ctypes.data, m.ctypes.data, 0xFF)
         self.trust = True
 
     def step(self, actions, autoreset=True):
