@@ -290,7 +290,10 @@ struct ListStore {
 // runs out (FL_OVF from the list machinery) is not written back: the env goes
 // to the spill queue and spill_kernel re-runs the step on WsSerialBig.
 constexpr int kCap128 = 64;              // lane-0 list capacity of the <= 128-cell general kernels (cells)
-constexpr int kCap512 = 128;             // lane-0 list capacity of the 512-cell general kernels (cells)
+#ifndef TMG_CAP512
+#define TMG_CAP512 80
+#endif
+constexpr int kCap512 = TMG_CAP512;      // lane-0 list capacity of the 512-cell general kernels (cells)
 template <int MAXN, int CAP = (MAXN > 128 ? kCap512 : kCap128)>
 using WsSerial = ListStore<4 * CAP + 256, CAP + 64, 2 * CAP + 64, CAP + 32, 4 * CAP + 256, CAP + 8>;
 
