@@ -290,10 +290,13 @@ struct ListStore {
 // runs out (FL_OVF from the list machinery) is not written back: the env goes
 // to the spill queue and spill_kernel re-runs the step on WsSerialBig.
 constexpr int kCap128 = 64;              // lane-0 list capacity of the <= 128-cell general kernels (cells)
-#ifndef TMG_CAP512
-#define TMG_CAP512 80
-#endif
-constexpr int kCap512 = TMG_CAP512;      // lane-0 list capacity of the 512-cell general kernels (cells)
+// lane-0 list capacity of the 512-cell general kernels (cells): at 80 the
+// general workspace is 10 048 B, so 16 waves fit a CU's LDS and the
+// specialised c5 step kernel runs at its VGPR occupancy (4 waves/SIMD); at 128
+// (12 064 B) LDS held it to 13 waves per CU.  c5 1.56 -> 1.61 x 10^8
+// (profiles/r04/s9); a step that outgrows the lists re-runs exactly in the
+// spill tier.
+constexpr int kCap512 = 80;
 template <int MAXN, int CAP = (MAXN > 128 ? kCap512 : kCap128)>
 using WsSerial = ListStore<4 * CAP + 256, CAP + 64, 2 * CAP + 64, CAP + 32, 4 * CAP + 256, CAP + 8>;
 
