@@ -10,7 +10,9 @@
 // On the device a batch of M 32-bit draws is produced lane-parallel by
 // jump-ahead: lane j computes s_{j+1} = A^{j+1} s + G_{j+1} inc
 // (G_j = sum_{i<j} A^i) from a 64-entry table built on the host, so one
-// wave64 round yields 64 outputs = 128 uint32 draws.
+// wave64 round yields 64 outputs = 128 uint32 draws.  The row-plane generate
+// (tmg_board.hip, bp_*) then advances each lane by 64 outputs at a time
+// (A^64, G_64) and recovers an exact position by a backward jump (rows 64..71).
 #pragma once
 #include <stdint.h>
 
@@ -54,7 +56,11 @@ __host__ __device__ __forceinline__ U128 add128(U128 a, U128 b) {
 }
 
 // s = A * f + g (mod 2^128): the jump-ahead s_j = A^j s + G_j inc of a lane
-// (A, g per lane, f = the wave-uniform stream state, in SGPRs).  Device: ten
+// (A, g per lane, f = the wave-uniform stream state, in SGPRs; or X, A^64,
+// G_64 inc of the row-plane generate's lane-local batches).  f MUST be
+// wave-uniform: its limbs are "s" operands, and for a value the compiler
+// holds in VGPRs it inserts a v_readfirstlane, i.e. every lane would get lane
+// 0's f.  Device: ten
 // v_mad_u64_u32, whose 64-bit addends carry the next limb's partial sum and
 // whose carry-outs (SGPR masks) are added back with v_addc: the 32-bit limbs
 // r0..r3 of the result are
@@ -113,7 +119,11 @@ __host__ __device__ __forceinline__ uint64_t xsl_rr(U128 s) {
 static constexpr uint64_t PCG_A_LO = 0x4385DF649FCCF645ULL;
 static constexpr uint64_t PCG_A_HI = 0x2360ED051FC65DA4ULL;
 
-// Host: jump table [64][4] = {A^j lo, A^j hi, G_j lo, G_j hi} for j = 1..64.
+// Host: jump table [kJumpRows][4]:
+//   rows 0..63:  {A^j lo, A^j hi, G_j lo, G_j hi} for j = 1..64 (s_j = A^j s + G_j inc);
+//   rows 64..71: {B lo, B hi, D lo, D hi} with B = A^{-64m}, D = -A^{-64m} G_{64m}
+//                for m = 1..8, so s = B s_{64m} + D inc (64m outputs back).
+constexpr int kJumpRows = 72;
 inline void build_jump_table(uint64_t *tab) {
     U128 A{PCG_A_LO, PCG_A_HI};
     U128 Aj{1, 0}, Gj{0, 0};
@@ -124,6 +134,26 @@ inline void build_jump_table(uint64_t *tab) {
         tab[(j - 1) * 4 + 1] = Aj.hi;
         tab[(j - 1) * 4 + 2] = Gj.lo;
         tab[(j - 1) * 4 + 3] = Gj.hi;
+    }
+    // A^{-1} mod 2^128 (A odd) by Newton's iteration x <- x (2 - A x): A x = 1
+    // mod 2^3 for x = A, each step doubles the exact low bits
+    U128 inv = A;
+    for (int it = 0; it < 6; it++) {
+        const U128 ax = mul128(A, inv);
+        inv = mul128(inv, add128(U128{2, 0}, U128{~ax.lo + 1, ~ax.hi + (ax.lo == 0 ? 1ULL : 0ULL)}));
+    }
+    const U128 A64{tab[63 * 4], tab[63 * 4 + 1]}, G64{tab[63 * 4 + 2], tab[63 * 4 + 3]};
+    U128 Gm{0, 0}, Binv{1, 0};                      // G_{64m}, A^{-64m}
+    U128 inv64{1, 0};
+    for (int j = 0; j < 64; j++) inv64 = mul128(inv64, inv);
+    for (int m = 1; m <= 8; m++) {
+        Gm = add128(mul128(A64, Gm), G64);          // G_{64m} = A^64 G_{64(m-1)} + G_64
+        Binv = mul128(Binv, inv64);
+        const U128 d = mul128(Binv, Gm);
+        tab[(63 + m) * 4 + 0] = Binv.lo;
+        tab[(63 + m) * 4 + 1] = Binv.hi;
+        tab[(63 + m) * 4 + 2] = ~d.lo + 1;          // -d mod 2^128
+        tab[(63 + m) * 4 + 3] = ~d.hi + (d.lo == 0 ? 1ULL : 0ULL);
     }
 }
 

@@ -1016,9 +1016,16 @@ __device__ __forceinline__ int generate_board(const Params &P, WS &w, int lane, 
 // hands lane r its C colours [cons + rC, cons + rC + C) as one funnel shift
 // (v_alignbit) of two ring dwords per plane.  Batches start at multiples of
 // 128 (a buffered half-word, the sequence's first colour, sits at index 127),
-// so a batch's planes are four whole dwords each, and its starting PCG64
-// state goes to one of 8 LDS slots, from which the exact stream position is
-// recovered at the end.
+// so a batch's planes are four whole dwords each.
+//
+// The batches advance lane-locally: lane l holds the PCG64 state X of its
+// output bp_out(l) of the next batch, and a fill takes that output and steps
+// X by 64 outputs, X <- A^64 X + G_64 inc (a wave-uniform multiplier), so a
+// batch's jump-ahead depends only on the lane's own previous one, not on a
+// readlane of the last lane, and it is issued before the batch's colours are
+// processed.  The exact stream position at the end is recovered from the
+// lane holding the last consumed colour by a backward jump of the batches
+// filled since (jump-table rows 64.., build_jump_table).
 constexpr int kBpRingDw = 32;                    // dwords per plane string (1024 colours)
 constexpr int kBpPlaneDw = 36;                   // + a guard copy of dwords 0..3, so [d, d+1] never wraps
 template <int NB>
@@ -1026,23 +1033,45 @@ struct RowPlanes {
     uint32_t p[NB];
 };
 struct BpRing {
-    U128 fs;                                     // wave-uniform: state after the last output filled
     int fill, cons, cons0;                       // colour indices: filled, consumed, consumed at init
-    bool rej;                                    // a rejected word was drawn (wave-uniform)
+    uint32_t rmin;                               // per lane: the smallest Lemire low word filled (a
+                                                 // rejected word was drawn iff some lane's < thr)
 };
 template <class WS>
 __device__ __forceinline__ uint32_t *bp_ring(WS &w) { return reinterpret_cast<uint32_t *>(w.u.draw); }   // [4][36]
-template <class WS>
-__device__ __forceinline__ uint32_t *bp_slots(WS &w) { return reinterpret_cast<uint32_t *>(w.u.draw) + 4 * kBpPlaneDw; }   // [8][4]
+
+// The batch's lane order: lane l computes PCG64 output bp_out(l) of the batch
+// (outputs o and 32 + o on lanes 2o and 2o + 1), so that the codes of colours l
+// and 64 + l (output l >> 1 resp. 32 + (l >> 1), half l & 1) are on lane l or
+// its quad neighbour l ^ 1: one DPP swap each instead of a cross-lane gather.
+__device__ __forceinline__ int bp_out(int lane) { return (lane >> 1) + ((lane & 1) << 5); }
+__device__ __forceinline__ int bp_lane(int out) { return out < 32 ? 2 * out : 2 * (out - 32) + 1; }   // inverse
+struct BpJump {
+    U128 X;                                      // per lane: state after output bp_out(lane) of the next batch
+    U128 c64;                                    // G_64 inc (wave-uniform, kept in VGPRs: the multiply-add's addend)
+    U128 A64;                                    // A^64 (wave-uniform, SGPRs)
+};
+__device__ __forceinline__ BpJump load_bp_jump(const Params &P, const Rng &g) {
+    const uint64_t *t = P.jump + 63 * 4;                             // row 63: A^64, G_64
+    BpJump J;
+    J.A64 = U128{bcast64(t[0]), bcast64(t[1])};                    // loaded as VMEM (the kernel writes global
+                                                                     // memory): said uniform, so SGPRs
+    J.c64 = mul128(U128{g.ilo, g.ihi}, U128{t[2], t[3]});
+    uint32_t c[4] = {(uint32_t)J.c64.lo, (uint32_t)(J.c64.lo >> 32), (uint32_t)J.c64.hi, (uint32_t)(J.c64.hi >> 32)};
+#pragma unroll
+    for (int i = 0; i < 4; i++) TMG_OPAQUE_V(c[i]);                 // in VGPRs once, not copied per fill
+    J.c64 = U128{((uint64_t)c[1] << 32) | c[0], ((uint64_t)c[3] << 32) | c[2]};
+    J.X = U128{0, 0};
+    return J;
+}
 
 template <int NB, class WS>
-__device__ __forceinline__ void bp_ring_init(const Params &P, WS &w, int lane, const Rng &g, BpRing &r) {
-    r.fs = U128{g.slo, g.shi};
+__device__ __forceinline__ void bp_ring_init(const Params &P, WS &w, int lane, const Rng &g, BpRing &r, BpJump &J) {
     r.fill = r.cons = 0;
-    r.rej = false;
+    r.rmin = 0xffffffffu;
     if ((g.h >> 32) & 1) {                                   // the buffered half-word is colour 127
         const uint64_t m = (uint64_t)(uint32_t)g.h * (uint32_t)P.k;
-        r.rej = (uint32_t)m < P.thr;
+        r.rmin = (uint32_t)m;
         const uint32_t code = (uint32_t)(m >> 32);
         uint32_t *ring = bp_ring(w);
         if (lane == 0) {
@@ -1053,38 +1082,25 @@ __device__ __forceinline__ void bp_ring_init(const Params &P, WS &w, int lane, c
         r.fill = 128;
     }
     r.cons0 = r.cons;
+    // the first batch's states: s_{o+1} = A^{o+1} s + G_{o+1} inc, o = bp_out(lane)
+    // (an opaque lane: after a shuffle the loop calls this again, and the
+    // table row and its product with inc would otherwise be hoisted out of
+    // the loop and held in 8 VGPRs through every redraw)
+    const uint64_t *t = P.jump + bp_out(loop_lane(lane)) * 4;
+    J.X = jump128(U128{t[0], t[1]}, U128{g.slo, g.shi}, mul128(U128{g.ilo, g.ihi}, U128{t[2], t[3]}));
 }
 
-// The batch's lane order: lane l computes PCG64 output bp_out(l) of the batch
-// (outputs o and 32 + o on lanes 2o and 2o + 1), so that the codes of colours l
-// and 64 + l (output l >> 1 resp. 32 + (l >> 1), half l & 1) are on lane l or
-// its quad neighbour l ^ 1: one DPP swap each instead of a cross-lane gather.
-// Output 63, the next batch's starting state, stays on lane 63.
-__device__ __forceinline__ int bp_out(int lane) { return (lane >> 1) + ((lane & 1) << 5); }
-__device__ __forceinline__ int bp_lane(int out) { return out < 32 ? 2 * out : 2 * (out - 32) + 1; }   // inverse
-// A^{bp_out(lane)+1} and G_{bp_out(lane)+1} * inc (the LaneJump fields the fill uses)
-struct BpJump {
-    U128 Aj, incG;
-};
-__device__ __forceinline__ BpJump load_bp_jump(const Params &P, int lane, const Rng &g) {
-    const uint64_t *t = P.jump + bp_out(lane) * 4;
-    return BpJump{U128{t[0], t[1]}, mul128(U128{g.ilo, g.ihi}, U128{t[2], t[3]})};
-}
-
-// the next 128 colours (64 PCG64 outputs by jump-ahead, Lemire-32 on each
-// half) appended to the plane strings: lane l gets the codes of colours l and
-// 64 + l from itself and its quad neighbour, and one ballot per plane and half
-// gives the batch's bits in sequence order; lane 0 stores them and the
-// batch's starting state
+// the next 128 colours (64 PCG64 outputs, Lemire-32 on each half) appended
+// to the plane strings: lane l gets the codes of colours l and 64 + l from
+// itself and its quad neighbour, and one ballot per plane and half gives the
+// batch's bits in sequence order; lane 0 stores them
 template <int NB, class WS>
-__device__ __forceinline__ void bp_ring_fill(const Params &P, WS &w, int lane, const BpJump &J, BpRing &r) {
+__device__ __forceinline__ void bp_ring_fill(const Params &P, WS &w, int lane, BpJump &J, BpRing &r) {
     const uint32_t k = (uint32_t)P.k;
-    const U128 sj = jump128(J.Aj, r.fs, J.incG);
-    const uint64_t out = xsl_rr(sj);
+    const uint64_t out = xsl_rr(J.X);
+    J.X = jump128(J.X, J.A64, J.c64);                                // the next batch (A^64: uniform, SGPRs)
     const uint64_t m0 = (uint64_t)(uint32_t)out * k, m1 = (out >> 32) * k;
-    if (P.thr != 0u) {
-        if (__ballot(umin((uint32_t)m0, (uint32_t)m1) < P.thr) != 0ULL) r.rej = true;
-    }
+    if (P.thr != 0u) r.rmin = umin3(r.rmin, (uint32_t)m0, (uint32_t)m1);   // tested once, after the redraws
     const uint32_t c0 = (uint32_t)(m0 >> 32), c1 = (uint32_t)(m1 >> 32);   // codes of colours 2o, 2o + 1
     const uint32_t n0 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)c0, 0xb1, 0xf, 0xf, true);   // quad_perm [1,0,3,2]
     const uint32_t n1 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)c1, 0xb1, 0xf, 0xf, true);
@@ -1104,9 +1120,8 @@ __device__ __forceinline__ void bp_ring_fill(const Params &P, WS &w, int lane, c
     const int q = (r.fill >> 5) & (kBpRingDw - 1);
     if constexpr (WS::NP > 2) {
         // 512-cell kernels: one VGPR base (ring + q) for every store.  The
-        // planes, their guard copies and the batch's state slot (bp_slots +
-        // 4 * (fill >> 7 & 7) = ring + 144 + q) sit at immediate offsets from
-        // it, where separate scalar bases each needed a v_mov.  (The 128-cell
+        // planes and their guard copies sit at immediate offsets from it,
+        // where separate scalar bases each needed a v_mov.  (The 128-cell
         // kernels measured the same either way, profiles/r04/s8.)
         uint32_t *ws = reinterpret_cast<uint32_t *>(&w);
         int at = (int)(bp_ring(w) - ws) + q;                         // dword index of ring + q (scalar)
@@ -1125,8 +1140,6 @@ __device__ __forceinline__ void bp_ring_fill(const Params &P, WS &w, int lane, c
                     d[b * kBpPlaneDw / 2 + kBpRingDw / 2 + 1] = b1[b];
                 }
             }
-            d[2 * kBpPlaneDw] = r.fs.lo;                             // 4 * kBpPlaneDw dwords on
-            d[2 * kBpPlaneDw + 1] = r.fs.hi;
         }
     } else if (lane == 0) {
         uint32_t *ring = bp_ring(w);
@@ -1137,37 +1150,41 @@ __device__ __forceinline__ void bp_ring_fill(const Params &P, WS &w, int lane, c
             d[1] = b1[b];
             if (q == 0) { d[kBpRingDw / 2] = b0[b]; d[kBpRingDw / 2 + 1] = b1[b]; }   // guard copy
         }
-        uint64_t *slot = reinterpret_cast<uint64_t *>(bp_slots(w) + 4 * ((r.fill >> 7) & 7));
-        slot[0] = r.fs.lo;
-        slot[1] = r.fs.hi;
     }
     r.fill += 128;
-    r.fs = U128{rdlane64(sj.lo, 63), rdlane64(sj.hi, 63)};
 }
 
-// The exact PCG64 state after the last consumed colour: lane L of the batch
-// holding it, recomputed from that batch's starting state (its LDS slot).
-template <class WS>
-__device__ __forceinline__ void bp_ring_state(const BpJump &J, WS &w, const BpRing &r, Rng &g) {
+// Whether a filled word was Lemire-rejected (some lane's running minimum
+// below thr; a word filled but never consumed counts too, which only sends
+// the board to the exact path needlessly)
+__device__ __forceinline__ bool bp_rejected(const Params &P, const BpRing &r) {
+    return P.thr != 0u && __ballot(r.rmin < P.thr) != 0ULL;
+}
+
+// The exact PCG64 state after the last consumed colour i: lane L = the lane
+// of its output o holds X = s_{n+1} for output n = o of the next unfilled
+// batch, m = (fill >> 7) - (i >> 7) batches after i's (1 <= m <= 3: a take
+// leaves fewer than 256 colours filled ahead), so s = A^{-64m} X - A^{-64m}
+// G_{64m} inc (jump-table row 63 + m).
+__device__ __forceinline__ void bp_ring_state(const Params &P, const BpJump &J, const BpRing &r, Rng &g) {
     if (r.cons == r.cons0) return;                                   // nothing taken since bp_ring_init(g)
     const int i = r.cons - 1, local = i & 127;                       // i >= 128: a take draws >= 2 colours
-    WSYNC();
-    const uint32_t *st = bp_slots(w) + 4 * ((i >> 7) & 7);
-    const U128 b{((uint64_t)__builtin_amdgcn_readfirstlane(st[1]) << 32) | (uint32_t)__builtin_amdgcn_readfirstlane(st[0]),
-                 ((uint64_t)__builtin_amdgcn_readfirstlane(st[3]) << 32) | (uint32_t)__builtin_amdgcn_readfirstlane(st[2])};
-    const U128 sj = jump128(J.Aj, b, J.incG);
+    const int m = __builtin_amdgcn_readfirstlane((r.fill >> 7) - (i >> 7));
     const int l = bp_lane(local >> 1);
-    const U128 s{rdlane64(sj.lo, l), rdlane64(sj.hi, l)};
-    g.slo = s.lo;
-    g.shi = s.hi;
-    g.h = ((uint64_t)((local & 1) ^ 1) << 32) | (uint32_t)(xsl_rr(s) >> 32);   // lo half taken: hi half buffered
+    const U128 x{rdlane64(J.X.lo, l), rdlane64(J.X.hi, l)};
+    const uint64_t *t = P.jump + (63 + m) * 4;
+    const U128 s = add128(mul128(U128{bcast64(t[0]), bcast64(t[1])}, x),         // wave-uniform: SALU
+                          mul128(U128{bcast64(t[2]), bcast64(t[3])}, U128{g.ilo, g.ihi}));
+    g.slo = bcast64(s.lo);
+    g.shi = bcast64(s.hi);
+    g.h = ((uint64_t)((local & 1) ^ 1) << 32) | (uint32_t)(xsl_rr(U128{g.slo, g.shi}) >> 32);   // lo half taken: hi half buffered
 }
 
 // rows 0..row <- the ring's next (row + 1) * C colours (colour plane only)
 // AHEAD: the next redraw's batch is filled (when fewer than 128 colours would
 // be left) between issuing the ring reads and using them, under their latency
 template <int NB, bool AHEAD = false, class WS>
-__device__ __forceinline__ void bp_take(const Params &P, WS &w, int lane, const BpJump &J, BpRing &r, int row,
+__device__ __forceinline__ void bp_take(const Params &P, WS &w, int lane, BpJump &J, BpRing &r, int row,
                                         uint32_t cm, RowPlanes<NB> &pl) {
     const int M = (row + 1) * P.C;
     r.fill = __builtin_amdgcn_readfirstlane(r.fill);             // wave-uniform (see bp_generate)
@@ -1274,45 +1291,49 @@ __device__ __forceinline__ int bp_generate(const Params &P, WS &w, int lane, Rng
     // counters and state otherwise go to VGPRs and its loops run exec-masked
     rng_bcast(g);
     const Rng g0 = g;
-    const BpJump J = load_bp_jump(P, lane, g);
+    BpJump J = load_bp_jump(P, g);
     const uint32_t cm = C >= 32 ? ~0u : (1u << C) - 1u;
     const uint32_t hml = (lane < R && C >= 3) ? cm >> 2 : 0u;          // columns <= C-3
     const uint32_t vml = (lane >= 2 && lane < R) ? cm : 0u;            // rows >= 2
     for (int p = lane; p < N; p += 64) w.brd[N + p] = 1;
     BpRing r;
-    bp_ring_init<NB>(P, w, lane, g, r);
+    bp_ring_init<NB>(P, w, lane, g, r, J);
     RowPlanes<NB> pl;
 #pragma unroll
     for (int b = 0; b < NB; b++) pl.p[b] = 0;
     bp_take<NB>(P, w, lane, J, r, R - 1, cm, pl);                       // :97
     int fl = 0;
+    bool rej = false;
     for (int shuffles = 0;; shuffles++) {
-        for (;;) {                                                       // remove_colour_lines, :120-131
+        // remove_colour_lines, :120-131.  A Lemire rejection is looked for
+        // once the redraws end: until then the colours of a stream with a
+        // rejected word are still colours, the loop ends as it would on any
+        // other board, and the board is then redone exactly.
+        for (;;) {
             const int r0 = bp_first_line_row<NB>(pl, hml, vml);
             if (r0 < 0) break;
             bp_take<NB, true>(P, w, lane, J, r, R - 1 < r0 + 1 ? R - 1 : r0 + 1, cm, pl);   // rows 0..min(R-1, r0+1)
-            if (r.rej) break;
         }
-        if (r.rej) break;
+        if ((rej = bp_rejected(P, r))) break;
         bp_to_lds<NB>(P, w, lane, pl);
         WSYNC();
         if (scan_effective_clean<false>(P, w, lane)) break;             // possible_move, :102
         if (shuffles >= kMaxShuffles) { fl = FL_ERR; break; }
         COVER(CV_SHUFFLE_GEN);
-        bp_ring_state(J, w, r, g);                                       // shuffle draws from the stream itself
+        bp_ring_state(P, J, r, g);                                       // shuffle draws from the stream itself
         WSYNC();
         shuffle(P, w, lane, g);                                          // :105-106
         pl = bp_from_lds<NB>(P, w, lane);
         fl = FL_SHUF;
-        bp_ring_init<NB>(P, w, lane, g, r);
+        bp_ring_init<NB>(P, w, lane, g, r, J);
     }
-    if (r.rej) {
+    if (rej) {
         COVER(CV_REJECT_GEN);
         g = g0;
         WSYNC();
         return -1;
     }
-    bp_ring_state(J, w, r, g);
+    bp_ring_state(P, J, r, g);
     WSYNC();
     return fl & FL_ERR;
 }

@@ -282,7 +282,7 @@ bool shape_viable(int R, int C, int k) {
 
 int alloc_tables(tmg_ctx *c) {
     Params &P = c->P;
-    uint64_t tab[64 * 4];
+    uint64_t tab[tmg::kJumpRows * 4];
     tmg::build_jump_table(tab);
     int rc = hip_check(hipMalloc(&c->d_jump, sizeof tab), "hipMalloc");
     if (!rc) rc = hip_check(hipMemcpy(c->d_jump, tab, sizeof tab, hipMemcpyHostToDevice), "hipMemcpy");

@@ -1,7 +1,7 @@
 """Per-kernel register / scratch / occupancy table of libtmg's translation
 units, from the compiler's kernel-resource-usage remarks (diagnostics).
 
-    python tools/resource_usage.py [EXTRA_HIPCC_FLAGS ...]
+    python tools/resource_usage.py [EXTRA_HIPCC_FLAGS ...]     (TMG_TUS="4 5": those units only)
 """
 import os
 import re
@@ -27,12 +27,16 @@ def short(name):
 def main():
     extra = sys.argv[1:]
     rows = []
-    for tu in range(1, 8):
-        with tempfile.NamedTemporaryFile(suffix=".o") as f:
-            p = subprocess.run(["/opt/rocm/bin/hipcc", *FLAGS, *extra, f"-DTMG_TU={tu}", "-o", f.name,
-                                "csrc/tmg_kernels.hip"], cwd=PKG, capture_output=True, text=True)
+    tus = [int(t) for t in os.environ.get("TMG_TUS", "1 2 3 4 5 6 7").split()]
+    with tempfile.TemporaryDirectory() as tmp:          # the translation units compile in parallel
+        procs = [(tu, subprocess.Popen(["/opt/rocm/bin/hipcc", *FLAGS, *extra, f"-DTMG_TU={tu}", "-o",
+                                        os.path.join(tmp, f"k{tu}.o"), "csrc/tmg_kernels.hip"], cwd=PKG,
+                                       stderr=subprocess.PIPE, stdout=subprocess.DEVNULL, text=True))
+                 for tu in tus]
+        outs = [(tu, p.communicate()[1], p.returncode) for tu, p in procs]
+    for tu, err, rc in outs:
         cur = None
-        for line in p.stderr.splitlines():
+        for line in err.splitlines():
             m = re.search(r"remark: Function Name: (\S+)", line)
             if m:
                 cur = {"name": short(m.group(1)), "tu": tu}
@@ -42,8 +46,8 @@ def main():
                           r"SGPRs Spill|LDS Size \[bytes/block\]): (\d+)", line)
             if m and cur is not None:
                 cur[m.group(1).replace("SGPRs Spill", "SGPRsSpill").split()[0]] = int(m.group(2))
-        if p.returncode:
-            print(p.stderr[-3000:])
+        if rc:
+            print(err[-3000:])
             sys.exit(1)
     print(f"{'kernel':44s} {'TU':>2s} {'VGPR':>4s} {'SGPR':>4s} {'scr':>4s} {'occ':>3s} {'sspill':>6s}")
     for r in rows:

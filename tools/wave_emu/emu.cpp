@@ -229,7 +229,7 @@ static tmg::Params make_params(int R, int C, int k, int smask, int moves, const 
     return P;
 }
 
-static uint64_t g_jump[256];
+static uint64_t g_jump[tmg::kJumpRows * 4];
 static bool g_jump_init = false;
 
 static bool sb_ok(const tmg::Params &P) { return P.N <= 128 && P.C <= 63; }
