@@ -62,19 +62,45 @@ CONFIGS = {
 }
 
 
-# Profiled run shapes beyond the configs' defaults (tools/issue.py, tools/traffic.py
-# key their counts by these names): c4 = BASELINE configs[3], one GPU's shard of
-# 1 048 576 / 8 boards of the c2 shape.
+# Profiled runs (tools/issue.py, tools/traffic.py key their counts by these
+# names): a config name runs that config; c4 = BASELINE configs[3], one GPU's
+# shard of 1 048 576 / 8 boards of the c2 shape; a "-eff" suffix adds
+# --policy effective.
 PROFILE_RUNS = {"c4": ("c2", 131072)}
 
 
-def profile_key(config, boards):
-    """The profiles/*.json key of a run: its config name, or the PROFILE_RUNS
-    name of its (config, boards)."""
+def run_args(name):
+    """bench.py arguments of a profiled run name."""
+    base, eff = (name[:-4], True) if name.endswith("-eff") else (name, False)
+    cfg, boards = PROFILE_RUNS.get(base, (base, 0))
+    return ["--config", cfg] + (["--boards", str(boards)] if boards else []) + (["--policy", "effective"] if eff else [])
+
+
+def run_name(config, boards, policy):
+    """The profiled-run name of a bench line (the inverse of run_args)."""
+    base = config
     for name, (cfg, nb) in PROFILE_RUNS.items():
         if cfg == config and nb == boards:
-            return name
-    return config
+            base = name
+    return base + ("-eff" if policy == "effective" else "")
+
+
+def last_bench_line(path):
+    """The JSON line a bench run printed last (its log), or None."""
+    try:
+        with open(path) as f:
+            lines = [ln for ln in f if ln.startswith("{")]
+        return json.loads(lines[-1]) if lines else None
+    except (OSError, ValueError):
+        return None
+
+
+def run_identity(line):
+    """What a profile must share with a bench line to be attached to it: the
+    library build (source hash), the policy, the run shape and the API."""
+    c = line["config"]
+    return {"build_src": line["build"]["src"], "policy": c.get("policy", "uniform"), "api": c.get("api", "raw"),
+            "boards_per_gpu": c["boards_per_gpu"], "env_groups_per_gpu": c["env_groups_per_gpu"]}
 
 
 def workload_desc(R, C, k, nb, specials):
@@ -150,19 +176,20 @@ def cpu_baseline(config, R, C, k, smask, moves, policy="uniform"):
                                                 "(BASELINE.md §2); context only"}}
 
 
-def load_profile(name, config, boards, groups):
-    """The committed rocprofv3 counts of `config` (profiles/<name>), only if
-    they were taken on a run of the same shape (boards per GPU, env groups);
-    counts of another run shape would not describe this line's launches."""
-    p = os.path.join(ROOT, "profiles", name)
+def load_profile(fname, run, ident):
+    """The committed rocprofv3 counts of a profiled run (profiles/<fname>, key
+    `run`), only if they were taken on the same library build and run shape
+    (run_identity); counts of another build or shape would not describe this
+    line's launches."""
+    p = os.path.join(ROOT, "profiles", fname)
     if not os.path.exists(p):
         return None
     try:
         with open(p) as f:
-            prof = json.load(f).get(profile_key(config, boards))
+            prof = json.load(f).get(run)
     except Exception:
         return None
-    if not prof or prof.get("boards_per_gpu") != boards or prof.get("env_groups_per_gpu") != groups:
+    if not prof or any(prof.get(k) != v for k, v in ident.items()):
         return None
     return prof
 
@@ -204,6 +231,13 @@ def main():
                          "from step 0)")
     ap.add_argument("--phase-interleave", action="store_true",
                     help="env i in phase block i mod P (every env group holds all blocks) instead of contiguous blocks")
+    ap.add_argument("--api", default="raw", choices=("raw", "vector"),
+                    help="raw: TileMatchVecEnv.step_raw (headline); vector: the Gymnasium vector-env step "
+                         "(TileMatchVectorEnv.step: next-step autoreset, action masks, obs / reward / terminated / "
+                         "info tensors every step)")
+    ap.add_argument("--obs-dtype", default="int32", choices=("int32", "int8"),
+                    help="--api vector: the observation board dtype (int32 = the reference's, a converted copy; int8 = "
+                         "a view of the live state)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--dry-run", action="store_true", help="print each rank's shard layout and exit (no GPU)")
     args = ap.parse_args()
@@ -236,12 +270,26 @@ def main():
     from tile_match_gym_amd.vec_env import TileMatchVecEnv
     build = _native.build_info()            # the loader has checked the library against this tree's sources
     moves = 30
-    env = TileMatchVecEnv(nb, R, C, k, moves, cl, co, seeds=shard_seeds(rank, nb), device=dev, autoreset=True,
-                          groups=args.groups)
+    venv = None
+    if args.api == "vector":
+        from tile_match_gym_amd.vector import TileMatchVectorEnv
+        if args.policy != "uniform":
+            raise SystemExit("--api vector takes the uniform action stream (actions are the caller's)")
+        venv = TileMatchVectorEnv(nb, R, C, k, moves, cl, co, device=dev, autoreset_mode="next_step",
+                                  obs_dtype=torch.int32 if args.obs_dtype == "int32" else torch.int8,
+                                  action_masks=True, groups=args.groups)
+        venv.vec.set_seed(shard_seeds(rank, nb))
+        env = venv.vec
+    else:
+        env = TileMatchVecEnv(nb, R, C, k, moves, cl, co, seeds=shard_seeds(rank, nb), device=dev, autoreset=True,
+                              groups=args.groups)
     A = env.num_actions
     T = 300
     acts = torch.from_numpy(synthetic_actions(rng_, T, A)).to(dev)
-    env.reset()
+    if venv is not None:
+        venv.reset()
+    else:
+        env.reset()
     # --phase-align: move the reset schedule so that the timed window opens on a
     # block's reset step (the blocks' resets are `spacing` steps apart; any
     # window of a multiple of `spacing` steps holds the same reset work however
@@ -251,13 +299,15 @@ def main():
     shift = (moves - 1 - args.warmup) % spacing if (args.phase_align and args.phase_blocks > 1
                                                     and not args.phase_interleave) else 0
     if args.phase_blocks != 1:
-        env.stagger_phases(blocks=args.phase_blocks, first_env=rng_.start, interleave=args.phase_interleave,
-                           shift=shift)
+        (venv or env).stagger_phases(blocks=args.phase_blocks, first_env=rng_.start,
+                                     interleave=args.phase_interleave, shift=shift)
     env.status(clear=True)
 
     def step(t):
-        if args.policy == "effective":
-            env.step_effective(t, first_env=rng_.start)       # sampler + step, both on device
+        if venv is not None:
+            venv.step(acts[t % T])                            # obs, rewards, terminations, truncations, infos
+        elif args.policy == "effective":
+            env.step_effective(t, first_env=rng_.start)       # sampled inside the step kernel
         else:
             env.step_raw(acts[t % T])
 
@@ -313,7 +363,10 @@ def main():
         cpu = None if (args.no_cpu_baseline or world > 1) else cpu_baseline(args.config, R, C, k, smask, moves,
                                                                              policy=args.policy)
         issue = None
-        prof = load_profile("issue.json", args.config, nb, env.groups) if args.policy == "uniform" else None
+        ident = {"build_src": build["src"][:16], "policy": args.policy, "api": args.api, "boards_per_gpu": nb,
+                 "env_groups_per_gpu": env.groups}
+        run = run_name(args.config, nb, args.policy)
+        prof = load_profile("issue.json", run, ident)
         if prof:
             per_gpu = value / world
             v = prof["valu_per_env_step"] * per_gpu
@@ -323,7 +376,7 @@ def main():
                      "salu_peak": SALU_PEAK, "unit": "wave-instructions/s per GPU",
                      "valu_frac": round(v / VALU_PEAK, 4), "salu_frac": round(s / SALU_PEAK, 4),
                      "source": prof.get("source")}
-        traffic = load_profile("traffic.json", args.config, nb, env.groups) if args.policy == "uniform" else None
+        traffic = load_profile("traffic.json", run, ident)
         out = {
             "metric": METRIC,
             "value": round(value, 1),
@@ -348,9 +401,13 @@ def main():
                                            f"{moves // args.phase_blocks} steps"
                                            + (f", the timed window opening on a block's reset step (phases + {shift})"
                                               if shift else ""))
-                                   + ("" if args.policy == "uniform" else ", effective-action policy"),
+                                   + ("" if args.policy == "uniform" else ", effective-action policy")
+                                   + ("" if args.api == "raw" else
+                                      f", Gymnasium vector-env step (next-step autoreset, action masks, "
+                                      f"{args.obs_dtype} obs)"),
                        "boards_per_gpu": nb, "rows": R, "cols": C, "colours": k,
-                       "specials": cl + co, "env_groups_per_gpu": env.groups,
+                       "specials": cl + co, "env_groups_per_gpu": env.groups, "policy": args.policy,
+                       "api": args.api,
                        "parallelism": f"dp{world} (independent env shards, no collective)"},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 6),

@@ -102,6 +102,60 @@ TMG_API int tmg_step(tmg_ctx *ctx, int64_t n, int8_t *board, uint64_t *rng, int3
              const int32_t *actions, int32_t *reward, int32_t *n_new, int32_t *n_act,
              uint8_t *flags, uint64_t *eff, int trust_eff, int autoreset, void *stream);
 
+/* Step plans: one host call per batched step of a fixed set of buffers
+ * (TileMatchEnv.step, tile_match_env.py:93-124, for every env of the batch),
+ * with the batch split into env groups on their own streams, the callers'
+ * per-step outputs written in the kernels' own write-back, and optionally
+ * the examples' policy sampled inside the step.
+ *
+ * tmg_plan_create binds the state / output buffers (as for tmg_step) and
+ * `groups` contiguous env groups: group g = envs [bounds[g], bounds[g+1])
+ * (bounds[0] = 0, bounds[groups] = n), stepped on streams[g] (NULL: the
+ * stream of each tmg_plan_step / tmg_plan_join call).  The plan keeps
+ * the pointers; the caller keeps the buffers and streams alive until
+ * tmg_plan_destroy. */
+typedef struct tmg_plan tmg_plan;
+TMG_API int tmg_plan_create(tmg_plan **out, tmg_ctx *ctx, int64_t n, int8_t *board, uint64_t *rng, int32_t *timer,
+                            int32_t *reward, int32_t *n_new, int32_t *n_act, uint8_t *flags, uint64_t *eff,
+                            int groups, const int64_t *bounds, void *const *streams);
+
+/* What each tmg_plan_step does (default: autoreset 1, no policy, no extra
+ * outputs).
+ *   autoreset: 0 none (as tmg_step's 0); 1 same step (as tmg_step's 1);
+ *     2 next step (gymnasium.vector's default): an env whose episode ends is
+ *     left as with 0 (terminated, all-zero mask), and the next call resets it
+ *     (Board regenerated from its stream) instead of stepping it: its action
+ *     is ignored, reward / n_new / n_act / flags 0 but TMG_FLAG_RESET.
+ *   policy != 0: actions[] is an output: env i plays a uniform draw over its
+ *     effective actions, exactly tmg_sample_effective(key, first_env + i, t)
+ *     (src/examples/q_learning.py:19-25), sampled inside the step.
+ *   onehot / onehot_dtype: fused OneHotWrapper planes, as tmg_step_onehot.
+ *   terminated [n][4] bytes: terminated, is_combination_match, shuffled,
+ *     error (0/1 each; the reference's step info, tile_match_env.py:102-112).
+ *   action_mask [n][A] bytes: 0/1 of the effective-action bitmask (the
+ *     reference's info["effective_actions"] as a mask), kept up to date: a
+ *     call rewrites the rows whose mask changed.  The caller initialises it
+ *     (e.g. after tmg_reset) from the bitmask.
+ *   moves_left [n]: num_moves - timer after the call (tile_match_env.py:114-116).
+ *   final_board [n][2][R][C]: with autoreset 1, the board each env whose
+ *     episode ended had before its regeneration (rows of other envs untouched).
+ * Any output pointer may be NULL (not written). */
+TMG_API int tmg_plan_config(tmg_plan *plan, int autoreset, int policy, uint64_t key, int64_t first_env,
+                            void *onehot, int onehot_dtype, uint8_t *terminated, uint8_t *action_mask,
+                            int64_t *moves_left, int8_t *final_board);
+
+/* One step of every env: the group streams first wait for the work queued
+ * on `stream` (an event), then each group's launches are enqueued on its
+ * stream.  Nothing waits for them: call tmg_plan_join before reading the
+ * results on `stream`.  actions [n] (input, or the policy's output) must stay
+ * valid until then.  t: the step counter of the policy draw.  trust_eff: as
+ * tmg_step. */
+TMG_API int tmg_plan_step(tmg_plan *plan, int32_t *actions, int32_t t, int trust_eff, void *stream);
+
+/* `stream` waits for every group's queued work (events). */
+TMG_API int tmg_plan_join(tmg_plan *plan, void *stream);
+TMG_API int tmg_plan_destroy(tmg_plan *plan);
+
 /* Replaces TileMatchEnv._get_effective_actions (tile_match_env.py:118-124,
  * is_move_effective board.py:735-787) as a bitmask, ignoring the timer. */
 TMG_API int tmg_effective(tmg_ctx *ctx, int64_t n, const int8_t *board, uint64_t *eff, void *stream);

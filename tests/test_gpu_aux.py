@@ -93,54 +93,48 @@ def test_checkpoint_restore_continues_bit_exact(tmp_path):
             assert torch.equal(getattr(env, f), getattr(env2, f)), (t, f)
 
 
-def _oracle_reset_subset(o, idx):
-    """OracleBatch has no masked reset: regenerate the envs `idx` through a sub-batch."""
-    if len(idx) == 0:
-        return
-    sub = orc.OracleBatch(o.R, o.C, o.k, o.smask, o.num_moves, o.rng[idx].copy())
-    sub.reset()
-    o.board[idx], o.rng[idx], o.timer[idx], o.eff[idx] = sub.board, sub.rng, sub.timer, sub.eff
-
-
+@pytest.mark.parametrize("cfg", [(8, 8, 3, 14), (10, 10, 4, 0)])
+@pytest.mark.parametrize("groups", [1, 3])
 @pytest.mark.parametrize("mode", ["next_step", "same_step"])
-def test_vector_env_autoreset_modes(mode):
+def test_vector_env_autoreset_modes(mode, groups, cfg):
+    """TileMatchVectorEnv (gymnasium vector API) vs the oracle driven with the
+    same autoreset semantics (tests/vector_ref.py): obs, rewards, terminations,
+    infos, action masks, final boards — the general kernels (deferred resets)
+    and the lean ones (inline), on one and on three group streams."""
     from tile_match_gym_amd.vector import TileMatchVectorEnv
-    n, R, C, k, moves, sm = 256, 8, 8, 3, 6, 14
+    from vector_ref import VectorOracle
+    R, C, k, sm = cfg
+    n, moves = 256, 6
     cl, co = _lists(sm)
-    venv = TileMatchVectorEnv(n, R, C, k, moves, cl, co, seed=40, device=DEV, autoreset_mode=mode)
+    venv = TileMatchVectorEnv(n, R, C, k, moves, cl, co, seed=40, device=DEV, autoreset_mode=mode, groups=groups)
     ref = orc.OracleBatch(R, C, k, sm, moves, venv.vec.rng_words().copy())
     obs, info = venv.reset()
     ref.reset()
     assert np.array_equal(obs["board"].cpu().numpy(), ref.board.astype(np.int32))
     A = venv.single_action_space.n
     assert venv.action_space.shape == (venv.num_envs,) and (venv.action_space.nvec == A).all()
+    vo = VectorOracle(ref, mode)
     rs = np.random.default_rng(1)
-    pending = np.zeros(n, bool)
     for t in range(3 * moves + 2):
         a = rs.integers(0, A, n).astype(np.int32)
         obs, rew, term, trunc, info = venv.step(torch.from_numpy(a).to(DEV))
-        if mode == "next_step":
-            live = ~pending
-            ref.step(a, autoreset=False)             # pending envs: step-after-done error, state untouched
-            _oracle_reset_subset(ref, np.nonzero(pending)[0])
-            want_term = ((ref.flags & 1) != 0) & live
-            want_rew = np.where(live, ref.reward, 0)
-            pending = want_term
-        else:
-            ref.step(a, autoreset=False)
-            want_term = (ref.flags & 1) != 0
-            want_rew = ref.reward
+        want = vo.step(a)
+        want_term = want["terminated"][:, 0].astype(bool)
+        if mode == "same_step":
             fb = info["final_obs"]["board"].cpu().numpy()
             assert np.array_equal(info["_final_obs"].cpu().numpy(), want_term)
-            assert np.array_equal(fb[want_term], ref.board[want_term].astype(np.int32))
-            _oracle_reset_subset(ref, np.nonzero(want_term)[0])
+            assert np.array_equal(fb[want_term], want["final_board"][want_term].astype(np.int32))
         assert np.array_equal(term.cpu().numpy(), want_term), t
         assert not trunc.any()
-        assert np.array_equal(rew.cpu().numpy(), want_rew), t
+        assert np.array_equal(rew.cpu().numpy(), want["reward"]), t
         assert np.array_equal(obs["board"].cpu().numpy(), ref.board.astype(np.int32)), t
-        assert np.array_equal(obs["num_moves_left"].cpu().numpy(), moves - ref.timer), t
-        mask = np.unpackbits(ref.eff.view(np.uint8).reshape(n, -1), axis=1, bitorder="little")[:, :A].astype(bool)
-        assert np.array_equal(info["action_mask"].cpu().numpy(), mask), t
+        assert np.array_equal(obs["num_moves_left"].cpu().numpy(), want["moves_left"]), t
+        for i, key in enumerate(("is_combination_match", "shuffled", "error")):
+            col = (1, 2, 3)[i]
+            assert np.array_equal(info[key].cpu().numpy(), want["terminated"][:, col].astype(bool)), (t, key)
+        assert np.array_equal(info["num_new_specials"].cpu().numpy(), want["n_new"]), t
+        assert np.array_equal(info["num_specials_activated"].cpu().numpy(), want["n_act"]), t
+        assert np.array_equal(info["action_mask"].cpu().numpy(), want["action_mask"].astype(bool)), t
 
 
 def test_onehot_wrapper_reference_vectors():

@@ -234,3 +234,71 @@ def test_masked_reset_subsets_emulated(emu_lib, cfg):
         got = getattr(e, f).reshape(n, -1)
         want = np.where(sel[:, None], getattr(o, f).reshape(n, -1), before[f].reshape(n, -1))
         assert np.array_equal(got, want), f"{cfg}: {f}"
+
+
+@pytest.mark.parametrize("cfg", [(10, 10, 4, 0), (8, 8, 3, 14), (7, 9, 5, 15), (12, 12, 5, 15)])
+@pytest.mark.parametrize("mode", ["next_step", "same_step"])
+def test_plan_vector_outputs_emulated(emu_lib, cfg, mode):
+    """tmg_plan_config's Gymnasium vector-env step (include/tmg.h): next-step
+    autoreset done by the kernels (inline for the lean kernels, by the masked
+    reset launch for the others), and the per-env outputs written in the
+    kernels' write-back — terminated / info bytes, action-mask bytes (kept
+    across steps: rows rewritten only where the mask changes), moves left,
+    same-step final boards — against the oracle driven with the same semantics."""
+    from oracle import oracle as orc
+    from tile_match_gym_amd.seeding import batch_rng_words
+    from vector_ref import VectorOracle, mask_bytes
+    emu, L = emu_lib
+    R, C, k, sm = cfg
+    n, moves = 12, 5
+    A = 2 * R * C - R - C
+    w = batch_rng_words(range(700, 700 + n))
+    e = emu.EmuBatch(L, R, C, k, sm, moves, w)
+    o = orc.OracleBatch(R, C, k, sm, moves, w)
+    e.reset()
+    o.reset()
+    ref = VectorOracle(o, mode)
+    outs = {"terminated": np.zeros((n, 4), np.uint8), "action_mask": mask_bytes(e.eff, A),
+            "moves_left": np.full(n, moves, np.int64), "final_board": np.zeros((n, 2, R, C), np.int8)}
+    rs = np.random.default_rng(R + C + k + sm)
+    for t in range(3 * moves + 2):
+        a = rs.integers(0, A, n).astype(np.int32)
+        want = ref.step(a)
+        e.step(a, mode={"same_step": 1, "next_step": 2}[mode], outputs=outs)
+        for f in ("board", "rng", "eff", "timer"):
+            assert np.array_equal(getattr(e, f), getattr(o, f)), (cfg, mode, t, f)
+        for f in ("reward", "n_new", "n_act"):
+            assert np.array_equal(getattr(e, f), want[f]), (cfg, mode, t, f)
+        for f in ("terminated", "action_mask", "moves_left"):
+            assert np.array_equal(outs[f], want[f]), (cfg, mode, t, f)
+        if mode == "same_step":
+            term = want["terminated"][:, 0].astype(bool)
+            assert np.array_equal(outs["final_board"][term], want["final_board"][term]), (cfg, t)
+
+
+@pytest.mark.parametrize("cfg", [(10, 10, 4, 0), (8, 8, 3, 14), (12, 12, 5, 15)])
+def test_plan_policy_in_kernel_emulated(emu_lib, cfg):
+    """The examples' policy sampled inside the step kernel (tmg_plan_config
+    policy): the actions it writes equal tmg_sample_effective's draw
+    (oracle/policy_np.py) for the same (key, first_env, t), and the trajectory
+    equals the oracle stepping those actions."""
+    from oracle import oracle as orc
+    from oracle.policy_np import sample_effective_np
+    from tile_match_gym_amd.seeding import batch_rng_words
+    emu, L = emu_lib
+    R, C, k, sm = cfg
+    n, key, first = 10, 99, 1000
+    A = 2 * R * C - R - C
+    w = batch_rng_words(range(first, first + n))
+    e = emu.EmuBatch(L, R, C, k, sm, 7, w)
+    o = orc.OracleBatch(R, C, k, sm, 7, w)
+    e.reset()
+    o.reset()
+    acts = np.zeros(n, np.int32)
+    for t in range(20):
+        want = sample_effective_np(o.eff, A, key, first, t)
+        e.step(acts, True, policy=(key, first, t))
+        assert np.array_equal(acts, want), (cfg, t)
+        o.step(want, True)
+        for f in ("board", "rng", "eff", "reward", "flags", "timer", "n_new", "n_act"):
+            assert np.array_equal(getattr(e, f), getattr(o, f)), (cfg, t, f)

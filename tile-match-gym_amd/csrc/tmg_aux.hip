@@ -35,21 +35,14 @@ __global__ __launch_bounds__(256) void onehot_kernel(int64_t n, int N, int k, in
 // — the same stream as shard.synthetic_actions, so any shard layout picks the
 // same actions.  The r-th set bit, r = hi32(h) * count >> 32; with no
 // effective action (a finished env without autoreset) hi32(h) * A >> 32.
-// One thread per env; W <= 16 mask words.
-__device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
-    x += 0x9E3779B97F4A7C15ULL;
-    x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ULL;
-    x = (x ^ (x >> 27)) * 0x94D049BB133111EBULL;
-    return x ^ (x >> 31);
-}
-
+// One thread per env; W <= 16 mask words.  (The step kernel samples the same
+// way in its prologue, sample_action in tmg_board.hip, for tmg_step_groups.)
 __global__ __launch_bounds__(256) void sample_effective_kernel(int64_t n, int W, int A, const uint64_t *__restrict__ eff,
                                                                uint64_t key, int64_t first_env, int32_t t,
                                                                int32_t *__restrict__ actions) {
     const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
     if (i >= n) return;
-    const uint64_t base = splitmix64(key * 0xD1B54A32D192ED03ULL + (uint64_t)(first_env + i));
-    const uint64_t h = splitmix64(base ^ ((uint64_t)t * 0x9E3779B97F4A7C15ULL)) >> 32;
+    const uint64_t h = policy_draw(key, (uint64_t)(first_env + i), t);
     const uint64_t *m = eff + i * W;
     int count = 0;
     for (int j = 0; j < W; j++) count += __popcll(m[j]);

@@ -153,6 +153,20 @@ struct Params {
     SpillQ *spill;                // this launch's stream's spill queue (general kernels)
     void *spill_ws;               // kSpillWaves WsSerialBig<MAXN> for spill_kernel
     unsigned long long *cover;    // TMG_COVER builds: CV_COUNT hit counters (null otherwise)
+    // Gymnasium vector-env outputs of tmg_step_groups, written in the step's
+    // own write-back (each null unless asked for)
+    uint8_t *vo_term;             // [n][4] bytes: terminated, is_combination_match, shuffled, error
+    uint8_t *vo_mask;             // [n][A] bytes: the action mask (tile_match_env.py:118-124), rewritten
+                                  // only where the effective-action bitmask changes
+    int64_t *vo_left;             // [n]: num_moves_left after the call (tile_match_env.py:114-116)
+    int8_t *vo_final;             // [n][2][R][C]: same-step autoreset, the last board of each env whose
+                                  // episode ended, before its regeneration
+    // in-kernel policy (tmg_step_groups with a policy key): actions[e] <- uniform
+    // over env e's effective actions, the stream of tmg_sample_effective
+    int sample;
+    int32_t pol_t;
+    int64_t pol_first;            // global index of env 0 of the launch
+    uint64_t pol_key;
 };
 
 // The kernels take Params by value as their FIRST argument and read it
@@ -201,6 +215,14 @@ inline Params make_params(int R, int C, int k, int smask, int num_moves, const u
     P.oh = nullptr;
     P.oh_dtype = P.oh_ch = P.oh_nsel = 0;
     P.oh_sel = 0;
+    P.vo_term = nullptr;
+    P.vo_mask = nullptr;
+    P.vo_left = nullptr;
+    P.vo_final = nullptr;
+    P.sample = 0;
+    P.pol_t = 0;
+    P.pol_first = 0;
+    P.pol_key = 0;
     if (P.N <= 128) {
         for (int p = 0; p < P.N; p++) {
             const int c = p % C, w = p & 1, b = p >> 1;
@@ -559,6 +581,81 @@ __device__ __forceinline__ void store_onehot(const Params &P, const WS &w, int l
             else o32[c * N + p] = on ? one : 0u;
         }
     }
+}
+
+// The action mask bytes of env e (Params::vo_mask, [n][A] bools): byte a =
+// bit a of the effective-action bitmask in LDS (w.effw), or all zero.  Four
+// actions per lane and dword store when A is a multiple of 4: the nibble's
+// bits spread to the low bit of each byte by one multiply.
+template <class WS>
+__device__ __forceinline__ void store_mask(const Params &P, const WS &w, int lane, int64_t e, bool zero) {
+    const int A = P.A;
+    uint8_t *m = P.vo_mask + e * (int64_t)A;
+    if ((A & 3) == 0) {
+        uint32_t *m4 = reinterpret_cast<uint32_t *>(m);
+        for (int i = lane; i < (A >> 2); i += 64) {
+            const uint32_t b = zero ? 0u : (uint32_t)(w.effw[i >> 4] >> ((4 * i) & 63)) & 0xFu;
+            m4[i] = (b * 0x00204081u) & 0x01010101u;
+        }
+    } else {
+        for (int i = lane; i < A; i += 64) m[i] = zero ? (uint8_t)0 : (uint8_t)((w.effw[i >> 6] >> (i & 63)) & 1ULL);
+    }
+}
+
+// Per-env outputs of tmg_step_groups besides the step's own (lane 0)
+__device__ __forceinline__ void store_vo(const Params &P, int64_t e, int flags, int tnew) {
+    if (P.vo_term) {
+        const uint32_t v = ((flags & FL_DONE) ? 1u : 0u) | ((flags & FL_COMBO) ? 1u << 8 : 0u) |
+                           ((flags & FL_SHUF) ? 1u << 16 : 0u) | ((flags & FL_ERR) ? 1u << 24 : 0u);
+        reinterpret_cast<uint32_t *>(P.vo_term)[e] = v;
+    }
+    if (P.vo_left) P.vo_left[e] = (int64_t)(P.num_moves - tnew);
+}
+
+// The examples' policy (src/examples/q_learning.py:19-25), counter-based:
+// h = splitmix64(splitmix64(key K + global env) ^ t G) >> 32 (shard.synthetic_actions'
+// stream), shared by sample_effective_kernel and the step kernel's own
+// sampling (sample_action)
+__host__ __device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
+    x += 0x9E3779B97F4A7C15ULL;
+    x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ULL;
+    x = (x ^ (x >> 27)) * 0x94D049BB133111EBULL;
+    return x ^ (x >> 31);
+}
+__host__ __device__ __forceinline__ uint64_t policy_draw(uint64_t key, uint64_t gid, int32_t t) {
+    const uint64_t base = splitmix64(key * 0xD1B54A32D192ED03ULL + gid);
+    return splitmix64(base ^ ((uint64_t)t * 0x9E3779B97F4A7C15ULL)) >> 32;
+}
+
+// tmg_sample_effective's draw for env e inside the step (Params::sample):
+// the r-th set bit of the env's mask, r = h * count >> 32, or h * A >> 32 when
+// no action is effective.  effrow: lane i holds mask word i (W <= 64).
+// Wave-uniform, on the scalar unit: the words by readlane, the r-th set bit of
+// the chosen word by a binary search on popcounts.
+__device__ __forceinline__ int sample_action(const Params &P, uint64_t effrow, int64_t e) {
+    const uint64_t h = policy_draw(P.pol_key, (uint64_t)(P.pol_first + e), P.pol_t);
+    const int W = P.W;
+    int count = 0;
+    for (int j = 0; j < W; j++) count += __popcll(rdlane64(effrow, j));
+    if (count == 0) return (int)((h * (uint64_t)P.A) >> 32);
+    int r = (int)((h * (uint64_t)count) >> 32);
+    int a = 0;
+    for (int j = 0; j < W; j++) {
+        uint64_t x = rdlane64(effrow, j);
+        const int c = __popcll(x);
+        if (r < c) {
+            int pos = 0;
+#pragma unroll
+            for (int s = 32; s >= 1; s >>= 1) {
+                const int cl = __popcll(x & ((1ULL << s) - 1ULL));
+                if (r >= cl) { r -= cl; x >>= s; pos += s; }
+            }
+            a = j * 64 + pos;
+            break;
+        }
+        r -= c;
+    }
+    return a;
 }
 
 // is_move_effective, board.py:735-787 — exact windowed scan (any board)
@@ -2172,11 +2269,16 @@ __device__ __forceinline__ void store_rng(uint64_t *p, const Rng &g, int lane) {
 // GEN=false: lean variant for boards that can hold no special (no specials
 // enabled, cached effective mask trusted).  SBNB > 0 (<= 128 cells): the
 // scalar-bitboard path of tmg_sb.hip with SBNB colour planes (the move in the
-// lean variant, board generation in both); CODD = C is odd.  autoreset: 1
-// regenerates a finished board here, 2 leaves it to a following reset_kernel
-// launch masked by FL_RESET (the 512-cell kernels: the reset kernel's
-// occupancy is far higher than the general step kernel's).  Returns the ST_*
-// bits this step raises for the sticky status word.
+// lean variant, board generation in both); CODD = C is odd.  autoreset:
+//   0  none: an ended env writes an all-zero mask, a further step is an error;
+//   1  same step, inline: the env whose episode ends is regenerated here;
+//   2  same step, deferred: a following reset_kernel launch masked by
+//      FL_RESET regenerates it (the general and 512-cell kernels: the reset
+//      kernel's occupancy is far higher than theirs);
+//   3 / 4  next step (gymnasium's default), inline / deferred: an ending env
+//      is left as with 0, and the call after it regenerates it instead of
+//      stepping (its action ignored, reward 0, not terminated).
+// Returns the ST_* bits this step raises for the sticky status word.
 template <int MAXN, bool GEN, int SBNB, bool CODD, int TIER = TIER_MAIN, class WS = Ws<MAXN, GEN>,
           class L = WsSerial<MAXN>>
 __device__ __forceinline__ uint32_t step_env(
@@ -2186,11 +2288,14 @@ __device__ __forceinline__ uint32_t step_env(
     int autoreset, L *lists) {
     const int N = P.N, W = P.W;
     // Only the 128-cell lean kernels regenerate a finished board inline
-    // (autoreset == 1); do_step (tmg_capi.hip) hands every other kernel
-    // autoreset == 2, a masked reset_kernel launch after the step, so they
+    // (autoreset 1 / 3); do_step (tmg_capi.hip) hands every other kernel
+    // autoreset 2 / 4, a masked reset_kernel launch after the step, so they
     // carry no generate_board code
     constexpr bool INLINE_GEN = !GEN && MAXN == 128;
-    const int a = __builtin_amdgcn_readfirstlane(actions[e]);             // wave-uniform loads
+    const bool same = autoreset == 1 || autoreset == 2;
+    const bool regen_inline = autoreset == 1 || autoreset == 3;
+    int a = 0;
+    if (!P.sample) a = __builtin_amdgcn_readfirstlane(actions[e]);       // wave-uniform loads
     const int t0 = __builtin_amdgcn_readfirstlane(timer[e]);
     // Issued beside the two loads above, not depending on the action: the
     // env's cached mask row (lane i holds word i).  The ineffective-move exit
@@ -2200,8 +2305,16 @@ __device__ __forceinline__ uint32_t step_env(
     // state there too measured slower: the quick waves wait for those loads.
     const uint64_t effrow = lane < W ? eff[e * W + lane] : 0ULL;
     TMG_KEEP_V(effrow);
-    if (t0 >= P.num_moves || a < 0 || a >= P.A) {                           // tile_match_env.py:94-95
-        if (lane == 0) { reward[e] = 0; n_new[e] = 0; n_act[e] = 0; flags_out[e] = FL_ERR; }
+    if (P.sample) {                                                         // the policy's action, from the mask
+        a = __builtin_amdgcn_readfirstlane(sample_action(P, effrow, e));
+        if (lane == 0) const_cast<int32_t *>(actions)[e] = a;
+    }
+    const bool pend = autoreset >= 3 && t0 >= P.num_moves;                 // ended last call: reset() now
+    if (!pend && (t0 >= P.num_moves || a < 0 || a >= P.A)) {                // tile_match_env.py:94-95
+        if (lane == 0) {
+            reward[e] = 0; n_new[e] = 0; n_act[e] = 0; flags_out[e] = FL_ERR;
+            store_vo(P, e, FL_ERR, t0);
+        }
         if (P.oh && !trust_eff) {             // the fused planes follow every board of an untrusted call
             load_board(P, w, lane, board + e * 2 * N);
             WSYNC();
@@ -2212,18 +2325,32 @@ __device__ __forceinline__ uint32_t step_env(
     int8_t *gb = board + e * 2 * N;
     uint64_t *ge = eff + e * W;
     const int t1 = t0 + 1;
-    const bool done = t1 == P.num_moves;                                    // tile_match_env.py:100-101
+    const bool done = !pend && t1 == P.num_moves;                           // tile_match_env.py:100-101
+    // envs regenerated in this call (here or by the reset launch after it)
+    const bool regen = pend || (done && same);
     int flags = done ? FL_DONE : 0;
     bool effective = false;
-    if (trust_eff) {                                                        // board.py:352 via cached mask
+    if (trust_eff && !pend) {                                               // board.py:352 via cached mask
         effective = (rdlane64(effrow, a >> 6) >> (a & 63)) & 1ULL;
     }
-    if (trust_eff && !effective && !(done && autoreset == 1)) {             // no state change at all
-        const bool defer = done && autoreset;                               // autoreset == 2: reset_kernel next
-        if (done && !defer) for (int i = lane; i < W; i += 64) ge[i] = 0ULL; // tile_match_env.py:119-120
+    if (trust_eff && !effective && !(regen && regen_inline)) {              // no state change at all
+        const bool defer = regen;                                           // reset_kernel next
+        if (done && !same) {                                                // tile_match_env.py:119-120
+            for (int i = lane; i < W; i += 64) ge[i] = 0ULL;
+            if (P.vo_mask) store_mask(P, w, lane, e, true);
+        }
+        if (done && same && P.vo_final) {                                   // the last board, as it stands
+            const int nbw = (2 * N) >> 2;
+            const uint32_t *src = reinterpret_cast<const uint32_t *>(gb);
+            uint32_t *dst = reinterpret_cast<uint32_t *>(P.vo_final + e * 2 * N);
+            for (int i = lane; i < nbw; i += 64) dst[i] = src[i];
+            for (int i = 4 * nbw + lane; i < 2 * N; i += 64) P.vo_final[e * 2 * N + i] = gb[i];
+        }
         if (lane == 0) {
-            timer[e] = defer ? 0 : t1; reward[e] = 0; n_new[e] = 0; n_act[e] = 0;
+            const int tn = defer ? 0 : t1;
+            timer[e] = tn; reward[e] = 0; n_new[e] = 0; n_act[e] = 0;
             flags_out[e] = (uint8_t)(flags | (defer ? FL_RESET : 0));
+            store_vo(P, e, flags, tn);
         }
         return 0;
     }
@@ -2256,11 +2383,14 @@ __device__ __forceinline__ uint32_t step_env(
         bool ok = true;
         for (int p = lane; p < N; p += 64) ok &= w.brd[N + p] == 1;
         if (__ballot(!ok) != 0ULL) {
-            if (lane == 0) { reward[e] = 0; n_new[e] = 0; n_act[e] = 0; flags_out[e] = FL_ERR; }
+            if (lane == 0) {
+                reward[e] = 0; n_new[e] = 0; n_act[e] = 0; flags_out[e] = FL_ERR;
+                store_vo(P, e, FL_ERR, t0);
+            }
             return ST_INTERNAL;
         }
     }
-    if (!trust_eff) {
+    if (!trust_eff && !pend) {
         bool ex = lane == 0 ? eff_exact(P, w.brd, a) : false;
         effective = __ballot(ex) != 0ULL;
     }
@@ -2294,9 +2424,10 @@ __device__ __forceinline__ uint32_t step_env(
         }
     }
     int tnew = t1;
-    if (done && autoreset) {                                                // reset() without a seed
+    if (regen) {                                                            // reset() without a seed
+        if (done && P.vo_final) store_board(P, w, lane, P.vo_final + e * 2 * N);   // same step: the last board
         if constexpr (INLINE_GEN) {
-            if (autoreset == 1) {
+            if (regen_inline) {
                 int fg = -1;
                 if constexpr (SBNB > 0) {
                     if (P.C <= 32) fg = bp_generate<SBNB>(P, w, lane, g);
@@ -2307,7 +2438,7 @@ __device__ __forceinline__ uint32_t step_env(
                 flags |= fg;
                 changed = true;
             }
-        }                                      // autoreset == 2: reset_kernel regenerates FL_RESET envs next
+        }                                      // autoreset 2 / 4: reset_kernel regenerates FL_RESET envs next
         tnew = 0;
         flags |= FL_RESET;
     }
@@ -2318,14 +2449,17 @@ __device__ __forceinline__ uint32_t step_env(
     // fused one-hot planes: every board this step changed (or, with an
     // untrusted mask, any board: it may have been edited by hand)
     if (P.oh && (changed || !trust_eff)) store_onehot(P, w, lane, e);
-    if (done && !autoreset) {
+    if (done && !same) {
         for (int i = lane; i < W; i += 64) ge[i] = 0ULL;                   // tile_match_env.py:119-120
+        if (P.vo_mask) store_mask(P, w, lane, e, true);
     } else if (changed) {
         for (int i = lane; i < W; i += 64) ge[i] = w.effw[i];
+        if (P.vo_mask) store_mask(P, w, lane, e, false);
     } else if (!trust_eff) {
         scan_effective(P, w, lane, cl, false);
         WSYNC();
         for (int i = lane; i < W; i += 64) ge[i] = w.effw[i];
+        if (P.vo_mask) store_mask(P, w, lane, e, false);
     }
     if (lane == 0) {
         timer[e] = tnew;
@@ -2333,6 +2467,7 @@ __device__ __forceinline__ uint32_t step_env(
         n_new[e] = nn;
         n_act[e] = na;
         flags_out[e] = (uint8_t)flags;
+        store_vo(P, e, flags, tnew);
     }
     return ((flags & FL_ERR) ? ST_INTERNAL : 0u) | ((flags & FL_OVF) ? ST_OVERFLOW : 0u);
 }
@@ -2488,7 +2623,11 @@ __device__ __forceinline__ void reset_env(const Params &P, WS &w, int lane, int6
     store_rng(rng + e * 5, g, lane);
     if (P.oh) store_onehot(P, w, lane, e);
     for (int i = lane; i < W; i += 64) eff[e * W + i] = w.effw[i];
-    if (lane == 0) timer[e] = 0;
+    if (P.vo_mask) store_mask(P, w, lane, e, false);
+    if (lane == 0) {
+        timer[e] = 0;
+        if (P.vo_left) P.vo_left[e] = P.num_moves;
+    }
 }
 
 template <int MAXN, int SBNB = 0, bool CODD = false, int FIX = kNoFix>

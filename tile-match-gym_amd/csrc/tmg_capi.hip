@@ -140,20 +140,22 @@ static int do_reset(tmg_ctx *ctx, const Params &P, int64_t n, int8_t *board, uin
     return hip_check(hipGetLastError(), "kernel launch");
 }
 
+// a.autoreset: 0 none, 1 same step, 2 next step (tmg_plan_config); the
+// kernels' codes are 1 / 3 inline and 2 / 4 deferred (step_env)
 static int do_step(tmg_ctx *ctx, Params P, StepArgs a, hipStream_t s) {
     // lean kernels: no special can exist (none enabled) and the cached mask
     // came from this library's own step / reset of the current boards
     const bool lean = ctx->P.smask == 0 && a.trust_eff;
     const dim3 grid = tmg::env_grid(a.n);
-    a.autoreset = a.autoreset ? 1 : 0;
+    const int mode = a.autoreset;
     // the general and 512-cell kernels leave finished boards to a reset launch
     // masked by FL_RESET, which runs at several times their occupancy
-    const int deferred = a.autoreset && (ctx->maxn == 512 || !lean);
+    const int deferred = mode && (ctx->maxn == 512 || !lean);
     if (!lean) {
         int rc = spill_for(ctx, s, a.n, &P.spill, &P.spill_ws);
         if (rc) return rc;
     }
-    if (deferred) a.autoreset = 2;
+    a.autoreset = mode == 0 ? 0 : mode == 1 ? (deferred ? 2 : 1) : (deferred ? 4 : 3);
     if (ctx->maxn == 128) {
         if (lean) tmg::launch_step_lean128(ctx->sb, grid, s, P, a);
         else if (ctx->sb && (P.C & 1)) tmg::launch_step_gen128_odd(grid, s, P, a);
@@ -469,8 +471,141 @@ int tmg_step_onehot(tmg_ctx *ctx, int64_t n, int8_t *board, uint64_t *rng, int32
     Params P;
     rc = onehot_params(ctx, onehot, onehot_dtype, P);
     if (rc) return rc;
-    const StepArgs a{n, board, rng, timer, actions, reward, n_new, n_act, flags, eff, trust_eff, autoreset};
+    const StepArgs a{n, board, rng, timer, actions, reward, n_new, n_act, flags, eff, trust_eff, autoreset ? 1 : 0};
     return do_step(ctx, P, a, reinterpret_cast<hipStream_t>(stream));
+}
+
+// ------------------------------------------------------------- step plans
+struct tmg_plan {
+    tmg_ctx *ctx;
+    int64_t n;
+    int8_t *board;
+    uint64_t *rng;
+    int32_t *timer, *reward, *n_new, *n_act;
+    uint8_t *flags;
+    uint64_t *eff;
+    std::vector<int64_t> bounds;          // groups + 1
+    std::vector<hipStream_t> streams;     // one per group
+    hipEvent_t fork;
+    std::vector<hipEvent_t> joins;
+    int autoreset, policy;
+    uint64_t key;
+    int64_t first_env;
+    Params P;                             // outputs of tmg_plan_config (one-hot, vector-env outputs)
+    size_t oh_env_bytes;
+};
+
+int tmg_plan_create(tmg_plan **out, tmg_ctx *ctx, int64_t n, int8_t *board, uint64_t *rng, int32_t *timer,
+                    int32_t *reward, int32_t *n_new, int32_t *n_act, uint8_t *flags, uint64_t *eff, int groups,
+                    const int64_t *bounds, void *const *streams) {
+    if (!out) return fail(-1, "null output pointer");
+    *out = nullptr;
+    if (!board || !rng || !timer || !reward || !n_new || !n_act || !flags || !eff) return fail(-1, "null buffer");
+    int rc = check_full(ctx, n);
+    if (rc) return rc;
+    if (groups < 1 || !bounds || !streams) return fail(-2, "a plan needs >= 1 group, its bounds and streams");
+    if (bounds[0] != 0 || bounds[groups] != n) return fail(-2, "group bounds must run from 0 to n");
+    for (int g = 0; g < groups; g++)
+        if (bounds[g + 1] < bounds[g]) return fail(-2, "group bounds must be non-decreasing");
+    tmg_plan *p = new tmg_plan();
+    p->ctx = ctx; p->n = n; p->board = board; p->rng = rng; p->timer = timer; p->reward = reward;
+    p->n_new = n_new; p->n_act = n_act; p->flags = flags; p->eff = eff;
+    p->bounds.assign(bounds, bounds + groups + 1);
+    for (int g = 0; g < groups; g++) p->streams.push_back(reinterpret_cast<hipStream_t>(streams[g]));
+    p->autoreset = 1; p->policy = 0; p->key = 0; p->first_env = 0;
+    p->P = ctx->P;
+    p->oh_env_bytes = 0;
+    rc = hip_check(hipEventCreateWithFlags(&p->fork, hipEventDisableTiming), "hipEventCreateWithFlags");
+    for (int g = 0; g < groups && !rc; g++) {
+        hipEvent_t ev;
+        rc = hip_check(hipEventCreateWithFlags(&ev, hipEventDisableTiming), "hipEventCreateWithFlags");
+        if (!rc) p->joins.push_back(ev);
+    }
+    if (rc) { tmg_plan_destroy(p); return rc; }
+    *out = p;
+    return 0;
+}
+
+int tmg_plan_config(tmg_plan *p, int autoreset, int policy, uint64_t key, int64_t first_env, void *onehot,
+                    int onehot_dtype, uint8_t *terminated, uint8_t *action_mask, int64_t *moves_left,
+                    int8_t *final_board) {
+    if (!p) return fail(-1, "null plan");
+    if (autoreset < 0 || autoreset > 2) return fail(-2, "autoreset must be 0 (none), 1 (same step) or 2 (next step)");
+    if (first_env < 0) return fail(-2, "first_env must be >= 0");
+    Params P;
+    int rc = onehot_params(p->ctx, onehot, onehot_dtype, P);
+    if (rc) return rc;
+    P.vo_term = terminated;
+    P.vo_mask = action_mask;
+    P.vo_left = moves_left;
+    P.vo_final = final_board;
+    P.sample = policy ? 1 : 0;
+    P.pol_key = key;
+    p->P = P;
+    p->oh_env_bytes = onehot ? (size_t)P.oh_ch * P.N * (P.oh_dtype == TMG_DTYPE_U8 ? 1 : 4) : 0;
+    p->autoreset = autoreset;
+    p->policy = policy ? 1 : 0;
+    p->key = key;
+    p->first_env = first_env;
+    return 0;
+}
+
+int tmg_plan_step(tmg_plan *p, int32_t *actions, int32_t t, int trust_eff, void *stream) {
+    if (!p) return fail(-1, "null plan");
+    if (!actions) return fail(-1, "null actions");
+    tmg_ctx *ctx = p->ctx;
+    int rc = set_device(ctx);
+    if (rc) return rc;
+    const hipStream_t cur = reinterpret_cast<hipStream_t>(stream);
+    const int G = (int)p->streams.size();
+    bool fork = false;                      // a NULL group stream is the call's own stream
+    for (int g = 0; g < G; g++) fork |= p->streams[g] != nullptr && p->streams[g] != cur;
+    if (fork) {                             // the group streams see the work queued on `stream`
+        rc = hip_check(hipEventRecord(p->fork, cur), "hipEventRecord");
+        for (int g = 0; g < G && !rc; g++)
+            if (p->streams[g] && p->streams[g] != cur)
+                rc = hip_check(hipStreamWaitEvent(p->streams[g], p->fork, 0), "hipStreamWaitEvent");
+        if (rc) return rc;
+    }
+    const int W = ctx->P.W, N = ctx->P.N, A = ctx->P.A;
+    for (int g = 0; g < G; g++) {
+        const int64_t lo = p->bounds[g], m = p->bounds[g + 1] - lo;
+        if (m <= 0) continue;
+        Params P = p->P;
+        if (P.oh) P.oh = static_cast<uint8_t *>(P.oh) + lo * p->oh_env_bytes;
+        if (P.vo_term) P.vo_term += 4 * lo;
+        if (P.vo_mask) P.vo_mask += lo * A;
+        if (P.vo_left) P.vo_left += lo;
+        if (P.vo_final) P.vo_final += lo * 2 * N;
+        P.pol_first = p->first_env + lo;
+        P.pol_t = t;
+        const StepArgs a{m, p->board + lo * 2 * N, p->rng + lo * 5, p->timer + lo, actions + lo, p->reward + lo,
+                         p->n_new + lo, p->n_act + lo, p->flags + lo, p->eff + lo * W, trust_eff, p->autoreset};
+        rc = do_step(ctx, P, a, p->streams[g] ? p->streams[g] : cur);
+        if (rc) return rc;
+    }
+    return 0;
+}
+
+int tmg_plan_join(tmg_plan *p, void *stream) {
+    if (!p) return fail(-1, "null plan");
+    int rc = set_device(p->ctx);
+    const hipStream_t cur = reinterpret_cast<hipStream_t>(stream);
+    const int G = (int)p->streams.size();
+    for (int g = 0; g < G && !rc; g++) {
+        if (!p->streams[g] || p->streams[g] == cur) continue;
+        rc = hip_check(hipEventRecord(p->joins[g], p->streams[g]), "hipEventRecord");
+        if (!rc) rc = hip_check(hipStreamWaitEvent(cur, p->joins[g], 0), "hipStreamWaitEvent");
+    }
+    return rc;
+}
+
+int tmg_plan_destroy(tmg_plan *p) {
+    if (!p) return 0;
+    if (p->fork) (void)hipEventDestroy(p->fork);
+    for (auto ev : p->joins) (void)hipEventDestroy(ev);
+    delete p;
+    return 0;
 }
 
 int tmg_effective(tmg_ctx *ctx, int64_t n, const int8_t *board, uint64_t *eff, void *stream) {
@@ -564,7 +699,7 @@ __attribute__((visibility("default"))) int tmg_debug_cover(tmg_ctx *ctx, uint64_
 int tmg_num_actions(const tmg_ctx *ctx) { return ctx ? ctx->P.A : -1; }
 int tmg_mask_words(const tmg_ctx *ctx) { return ctx ? ctx->P.W : -1; }
 const char *tmg_last_error(void) { return g_err.c_str(); }
-int tmg_abi_version(void) { return 3; }
+int tmg_abi_version(void) { return 4; }
 const char *tmg_build_info(void) { return "src=" TMG_SRC_SHA ";variant=" TMG_VARIANT; }
 
 }  // extern "C"

@@ -24,9 +24,10 @@ LIB_PATH = os.environ.get("TMG_LIB") or DEFAULT_LIB   # TMG_LIB: a diagnostic or
 EXPORTS = ("tmg_create", "tmg_create_scan", "tmg_destroy", "tmg_reset", "tmg_step", "tmg_effective",
            "tmg_num_actions", "tmg_mask_words", "tmg_last_error", "tmg_abi_version", "tmg_build_info",
            "tmg_onehot", "tmg_onehot_channels", "tmg_count_states", "tmg_sample_effective", "tmg_status",
-           "tmg_viable", "tmg_spills", "tmg_step_onehot", "tmg_reset_onehot")
+           "tmg_viable", "tmg_spills", "tmg_step_onehot", "tmg_reset_onehot", "tmg_plan_create", "tmg_plan_config",
+           "tmg_plan_step", "tmg_plan_join", "tmg_plan_destroy")
 DTYPE_F32, DTYPE_U8, DTYPE_I32 = 0, 1, 2
-ABI_VERSION = 3
+ABI_VERSION = 4
 STATUS_INTERNAL, STATUS_OVERFLOW, STATUS_CALLER = 1, 2, 4
 
 # CV_* branch counters of TMG_COVER builds (tmg_board.hip), in index order
@@ -83,10 +84,16 @@ def load(path: str = None):
     L.tmg_spills.argtypes = [P, ctypes.POINTER(ctypes.c_uint64)]
     L.tmg_step_onehot.argtypes = [P, I64, P, P, P, P, P, P, P, P, P, I, I, P, I, P]
     L.tmg_reset_onehot.argtypes = [P, I64, P, P, P, P, P, P, I, P]
+    L.tmg_plan_create.argtypes = [ctypes.POINTER(P), P, I64, P, P, P, P, P, P, P, P, I, P, P]
+    L.tmg_plan_config.argtypes = [P, I, I, ctypes.c_uint64, I64, P, I, P, P, P, P]
+    L.tmg_plan_step.argtypes = [P, P, ctypes.c_int32, I, P]
+    L.tmg_plan_join.argtypes = [P, P]
+    L.tmg_plan_destroy.argtypes = [P]
     for name in ("tmg_create", "tmg_create_scan", "tmg_destroy", "tmg_reset", "tmg_step", "tmg_effective",
                  "tmg_num_actions", "tmg_mask_words", "tmg_abi_version", "tmg_onehot", "tmg_onehot_channels",
                  "tmg_sample_effective", "tmg_status", "tmg_viable", "tmg_spills", "tmg_step_onehot", "tmg_reset_onehot",
-                 "tmg_count_states"):
+                 "tmg_count_states", "tmg_plan_create", "tmg_plan_config", "tmg_plan_step", "tmg_plan_join",
+                 "tmg_plan_destroy"):
         getattr(L, name).restype = I
     if L.tmg_abi_version() != ABI_VERSION:
         raise TmgError("libtmg.so ABI version mismatch; rebuild it")
@@ -221,6 +228,56 @@ class Context:
     def sample_effective(self, n, eff, key, first_env, t, actions, stream):
         self._check(self._L.tmg_sample_effective(self._h, int(n), eff, int(key) & 0xFFFFFFFFFFFFFFFF, int(first_env),
                                           int(t), actions, stream))
+
+
+class Plan:
+    """A tmg_plan: one host call per batched step of fixed buffers over env
+    groups on their own streams (include/tmg.h).  `bufs`: the state / output
+    tensors (board, rng, timer, reward, n_new, n_act, flags, eff); `bounds`:
+    group g = envs [bounds[g], bounds[g+1]); `streams`: raw hipStream_t per
+    group.  The caller keeps the buffers and streams alive."""
+
+    AUTORESET = {"none": 0, "same_step": 1, "next_step": 2}
+
+    def __init__(self, ctx: "Context", n, board, rng, timer, reward, n_new, n_act, flags, eff, bounds, streams):
+        L = self._L = ctx._L
+        self._ctx = ctx                      # the context outlives the plan
+        G = len(streams)
+        self._bounds = (ctypes.c_int64 * (G + 1))(*[int(b) for b in bounds])
+        self._streams = (P * G)(*[int(x) for x in streams])
+        h = P()
+        check(L.tmg_plan_create(ctypes.byref(h), ctx.handle, int(n), board, rng, timer, reward, n_new, n_act, flags,
+                                eff, G, self._bounds, self._streams), L)
+        self._h = h
+        self._step = L.tmg_plan_step
+        self._join = L.tmg_plan_join
+
+    def config(self, autoreset="same_step", policy=False, key=0, first_env=0, onehot=None, onehot_dtype=DTYPE_F32,
+               terminated=None, action_mask=None, moves_left=None, final_board=None):
+        check(self._L.tmg_plan_config(self._h, self.AUTORESET[autoreset], int(bool(policy)),
+                                      int(key) & 0xFFFFFFFFFFFFFFFF, int(first_env), onehot, int(onehot_dtype),
+                                      terminated, action_mask, moves_left, final_board), self._L)
+
+    def step(self, actions_ptr: int, t: int, trust_eff: int, stream: int):
+        rc = self._step(self._h, actions_ptr, t, trust_eff, stream)
+        if rc:
+            check(rc, self._L)
+
+    def join(self, stream: int):
+        rc = self._join(self._h, stream)
+        if rc:
+            check(rc, self._L)
+
+    def close(self):
+        if getattr(self, "_h", None) is not None and self._h.value:
+            self._L.tmg_plan_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
 
 
 _SCAN_CTX = {}

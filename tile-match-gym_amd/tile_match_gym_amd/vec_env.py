@@ -55,6 +55,16 @@ def _ptr(t: torch.Tensor):
     return t.data_ptr() if t is not None else None
 
 
+def _raw_stream(device_index: int) -> int:
+    """The current HIP stream of the device as a raw handle (the cheap accessor
+    when this torch has it)."""
+    return torch.cuda.current_stream(device_index).cuda_stream
+
+
+if hasattr(torch._C, "_cuda_getCurrentRawStream"):
+    _raw_stream = torch._C._cuda_getCurrentRawStream        # noqa: F811
+
+
 class TileMatchVecEnv:
     def __init__(self, num_envs: int, num_rows: int, num_cols: int, num_colours: int, num_moves: int,
                  colourless_specials=(), colour_specials=(), seed: int = 0, seeds=None, device=None,
@@ -97,18 +107,48 @@ class TileMatchVecEnv:
         bounds = [g * N // groups for g in range(groups + 1)]
         self._ranges = [(bounds[g], bounds[g + 1]) for g in range(groups) if bounds[g + 1] > bounds[g]]
         self._streams = [torch.cuda.Stream(device) for _ in self._ranges] if groups > 1 else []
-        self._ev_in = torch.cuda.Event() if groups > 1 else None
-        self._ev_out = [torch.cuda.Event() for _ in self._streams]
-        W, plane = self.mask_words, 2 * num_rows * num_cols
-        # per group: (n, board, rng, timer, eff, reward, n_new, n_act, flags) pointers
-        self._gptr = [(hi - lo, self.board.data_ptr() + lo * plane, self.rng.data_ptr() + lo * 40,
-                       self.timer.data_ptr() + lo * 4, self.eff.data_ptr() + lo * 8 * W,
-                       self.reward.data_ptr() + lo * 4, self.n_new.data_ptr() + lo * 4,
-                       self.n_act.data_ptr() + lo * 4, self.flags.data_ptr() + lo) for lo, hi in self._ranges]
+        # step plans (tmg_plan_*): one host call per batched step enqueues every
+        # group's launches with their fork event; one plan per action source
+        # (given actions / the in-kernel effective-action policy), configured
+        # with the attached outputs
+        bounds = [lo for lo, _ in self._ranges] + [N]
+        streams = [st.cuda_stream for st in self._streams] if self._streams else [0]
+        self._plans = {pol: _native.Plan(self.ctx, N, _ptr(self.board), _ptr(self.rng), _ptr(self.timer),
+                                         _ptr(self.reward), _ptr(self.n_new), _ptr(self.n_act), _ptr(self.flags),
+                                         _ptr(self.eff), bounds, streams) for pol in (False, True)}
+        self._policy = (12345, 0)                   # (key, first_env) the policy plan is configured with
+        self._vout = {}                             # extra outputs (set_step_outputs)
+        self._autoreset_mode = "same_step" if self.autoreset else "none"
+        self._held = []                             # action tensors the queued steps still read
+        self._dev_index = device.index if device.index is not None else torch.cuda.current_device()
+        self._configure()
 
     # ----------------------------------------------------------------- API
     def _stream(self):
-        return torch.cuda.current_stream(self.device).cuda_stream
+        return _raw_stream(self._dev_index)
+
+    def _configure(self):
+        """(Re)configure both step plans: autoreset mode, fused one-hot planes,
+        vector-env outputs, the policy's key and shard offset."""
+        for pol, plan in self._plans.items():
+            plan.config(self._autoreset_mode, policy=pol, key=self._policy[0], first_env=self._policy[1],
+                        onehot=_ptr(self.onehot), onehot_dtype=self._oh_code, **self._vout)
+
+    def set_step_outputs(self, autoreset_mode: str = None, terminated=None, action_mask=None, moves_left=None,
+                         final_board=None):
+        """Outputs every step writes in the kernels' own write-back (tmg_plan_config):
+        terminated (N, 4) uint8 (terminated, is_combination_match, shuffled, error),
+        action_mask (N, A) uint8/bool (kept up to date: rows are rewritten where the
+        mask changes, so initialise it after a reset), moves_left (N,) int64,
+        final_board (N, 2, R, C) int8 (same-step autoreset: the last board of each
+        env whose episode ended).  autoreset_mode: "none", "same_step", "next_step"."""
+        self.join()
+        if autoreset_mode is not None:
+            self._autoreset_mode = autoreset_mode
+        self._vout = {k: _ptr(v) for k, v in (("terminated", terminated), ("action_mask", action_mask),
+                                               ("moves_left", moves_left), ("final_board", final_board))}
+        self._vout_refs = (terminated, action_mask, moves_left, final_board)
+        self._configure()
 
     def set_seed(self, seeds):
         """Re-seed every env (== tile_match_env.py:79-82 per env)."""
@@ -164,12 +204,6 @@ class TileMatchVecEnv:
         self.join()
         return self.ctx.status(clear)
 
-    def _fork(self):
-        """Group streams wait for the work already queued on the current stream."""
-        self._ev_in.record(torch.cuda.current_stream(self.device))
-        for st in self._streams:
-            st.wait_event(self._ev_in)
-
     def record(self, event, group: int = 0):
         """Record `event` on the stream group `group` is stepped on (the current
         stream for groups=1): HIP-event timing of that group's launches."""
@@ -177,10 +211,9 @@ class TileMatchVecEnv:
 
     def join(self):
         """Make the current stream wait for every group's queued steps (no-op for groups=1)."""
-        cur = torch.cuda.current_stream(self.device)
-        for st, ev in zip(self._streams, self._ev_out):
-            ev.record(st)
-            cur.wait_event(ev)
+        if self._streams:
+            self._plans[False].join(self._stream())
+        self._held.clear()
 
     def reset(self, seed=None, env_mask=None):
         self.join()
@@ -219,27 +252,22 @@ class TileMatchVecEnv:
     def step_raw(self, actions_i32: torch.Tensor):
         """Enqueue one batched step (no output post-processing): the bench path.
         actions_i32: contiguous int32 (N,) on the device.  With groups > 1 call
-        join() before reading results."""
-        trust, auto = int(self._eff_valid), int(self.autoreset)
-        if not self._streams:
-            self.ctx.step(self.num_envs, _ptr(self.board), _ptr(self.rng), _ptr(self.timer), _ptr(actions_i32),
-                          _ptr(self.reward), _ptr(self.n_new), _ptr(self.n_act), _ptr(self.flags), _ptr(self.eff),
-                          trust, auto, self._stream(), self._oh(0), self._oh_code)
-        else:
-            self._fork()
-            a0 = actions_i32.data_ptr()
-            for (lo, _), st, p in zip(self._ranges, self._streams, self._gptr):
-                actions_i32.record_stream(st)
-                self.ctx.step(p[0], p[1], p[2], p[3], a0 + 4 * lo, p[5], p[6], p[7], p[8], p[4], trust, auto,
-                              st.cuda_stream, self._oh(lo), self._oh_code)
+        join() before reading results.  One host call (tmg_plan_step) enqueues
+        every group's launches; the actions tensor is held until join()."""
+        self._plans[False].step(actions_i32.data_ptr(), 0, int(self._eff_valid), self._stream())
         self._eff_valid = True
+        if self._streams:
+            self._held.append(actions_i32)
+            if len(self._held) > 256:
+                self.join()
 
     def step_effective(self, t: int, key: int = 12345, first_env: int = 0):
         """Enqueue one step of the examples' policy (src/examples/q_learning.py:19-25):
         every env takes an action drawn uniformly from its effective actions
-        (tmg_sample_effective; counter-based in (key, first_env + env, t), so a
-        shard passing its global offset as first_env picks the same actions as
-        the unsharded batch).  The sampled actions stay in self.actions."""
+        (tmg_sample_effective's draw, counter-based in (key, first_env + env, t),
+        so a shard passing its global offset as first_env picks the same actions
+        as the unsharded batch), sampled by the step kernel itself from the mask
+        it reads anyway.  The sampled actions stay in self.actions."""
         # a mask from tmg_effective (hand-edited boards) may sit beside a line
         # on the board, so that step runs untrusted (tmg.h, trust_eff)
         trust = int(self._eff_valid)
@@ -247,20 +275,11 @@ class TileMatchVecEnv:
             self.compute_effective()
         if self.actions is None:
             self.actions = torch.zeros(self.num_envs, dtype=torch.int32, device=self.device)
-        auto = int(self.autoreset)
-        act = self.actions.data_ptr()
-        if not self._streams:
-            s = self._stream()
-            self.ctx.sample_effective(self.num_envs, _ptr(self.eff), key, first_env, t, act, s)
-            self.ctx.step(self.num_envs, _ptr(self.board), _ptr(self.rng), _ptr(self.timer), act,
-                          _ptr(self.reward), _ptr(self.n_new), _ptr(self.n_act), _ptr(self.flags), _ptr(self.eff),
-                          trust, auto, s, self._oh(0), self._oh_code)
-        else:
-            self._fork()
-            for (lo, _), st, p in zip(self._ranges, self._streams, self._gptr):
-                self.ctx.sample_effective(p[0], p[4], key, first_env + lo, t, act + 4 * lo, st.cuda_stream)
-                self.ctx.step(p[0], p[1], p[2], p[3], act + 4 * lo, p[5], p[6], p[7], p[8], p[4], trust, auto,
-                              st.cuda_stream, self._oh(lo), self._oh_code)
+        if self._policy != (int(key), int(first_env)):
+            self.join()
+            self._policy = (int(key), int(first_env))
+            self._configure()
+        self._plans[True].step(self.actions.data_ptr(), int(t), trust, self._stream())
         self._eff_valid = True
 
     def invalidate_effective_cache(self):
@@ -295,6 +314,7 @@ class TileMatchVecEnv:
         self.onehot = torch.zeros((self.num_envs, ch, self.num_rows, self.num_cols), dtype=dtype, device=self.device)
         self._oh_code = codes[dtype]
         self.refresh_onehot()
+        self._configure()
         return self.onehot
 
     def refresh_onehot(self):
@@ -361,4 +381,7 @@ class TileMatchVecEnv:
         return env
 
     def close(self):
+        self.join()
+        for plan in self._plans.values():
+            plan.close()
         self.ctx.close()

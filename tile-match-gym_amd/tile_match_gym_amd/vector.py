@@ -23,6 +23,13 @@ batching follows gymnasium.vector.VectorEnv:
   ``action_mask`` — (N, A) bool of effective actions (tile_match_env.py:118-124;
   all False for a terminated env) — when ``action_masks=True``.
 * Truncation never happens in the reference (tile_match_env.py:112): all False.
+
+One host call per step (a tmg_plan step over the env groups' streams): the
+kernels themselves reset the envs due (next-step mode), keep the (N, A) mask
+bytes of the envs whose mask changed, and write the terminated / info bytes,
+moves left and (same-step mode) the final boards.  The returned tensors are
+views of the env's live buffers, overwritten by the next call; pass
+``copy=True`` for fresh tensors (gymnasium's vector-env ``copy`` flag).
 """
 from __future__ import annotations
 
@@ -39,7 +46,8 @@ class TileMatchVectorEnv:
 
     def __init__(self, num_envs: int, num_rows: int, num_cols: int, num_colours: int, num_moves: int,
                  colourless_specials=(), colour_specials=(), seed: int = 0, device=None,
-                 autoreset_mode: str = "next_step", obs_dtype=torch.int32, action_masks: bool = True):
+                 autoreset_mode: str = "next_step", obs_dtype=torch.int32, action_masks: bool = True,
+                 groups: int = 1, copy: bool = False):
         if autoreset_mode not in ("next_step", "same_step"):
             raise ValueError("autoreset_mode must be 'next_step' or 'same_step'")
         if obs_dtype not in (torch.int32, torch.int8):
@@ -48,8 +56,9 @@ class TileMatchVectorEnv:
         self.metadata = {"autoreset_mode": "NextStep" if autoreset_mode == "next_step" else "SameStep"}
         self.obs_dtype = obs_dtype
         self.action_masks = action_masks
+        self.copy = copy
         self.vec = TileMatchVecEnv(num_envs, num_rows, num_cols, num_colours, num_moves, colourless_specials,
-                                   colour_specials, seed=seed, device=device, autoreset=False)
+                                   colour_specials, seed=seed, device=device, autoreset=False, groups=groups)
         self.num_envs = num_envs
         self.device = self.vec.device
         self.num_moves = num_moves
@@ -68,75 +77,77 @@ class TileMatchVectorEnv:
                          shape=(num_envs, 2, R, C), dtype=np.int32),
             "num_moves_left": MultiDiscrete(np.full(num_envs, num_moves + 1, dtype=np.int64))})
         self.action_space = MultiDiscrete(np.full(num_envs, self.vec.num_actions, dtype=np.int64))
-        self._autoreset = torch.zeros(num_envs, dtype=torch.bool, device=self.device)
+        kw = dict(device=self.device)
+        A = self.vec.num_actions
+        # outputs the step kernels write (tmg_plan_config)
+        self._term = torch.zeros((num_envs, 4), dtype=torch.uint8, **kw)   # terminated, combo, shuffled, error
+        self._mask = torch.zeros((num_envs, A), dtype=torch.uint8, **kw) if action_masks else None
+        self._left = torch.zeros(num_envs, dtype=torch.int64, **kw)
+        self._final = (torch.zeros((num_envs, 2, R, C), dtype=torch.int8, **kw)
+                       if autoreset_mode == "same_step" else None)
+        self._trunc = torch.zeros(num_envs, dtype=torch.bool, **kw)
+        self._zero_left = torch.zeros(num_envs, dtype=torch.int64, **kw)
         self._bits = torch.arange(64, device=self.device, dtype=torch.int64)
+        self.vec.set_step_outputs(autoreset_mode, terminated=self._term, action_mask=self._mask,
+                                  moves_left=self._left, final_board=self._final)
 
     # ---------------------------------------------------------------- helpers
+    def _c(self, t):
+        return t.clone() if self.copy else t
+
+    def _board(self, b):
+        return self._c(b) if self.obs_dtype == torch.int8 else b.to(torch.int32)
+
     def _obs(self):
-        b = self.vec.board if self.obs_dtype == torch.int8 else self.vec.board.to(torch.int32)
-        return {"board": b, "num_moves_left": (self.num_moves - self.vec.timer).to(torch.int64)}
-
-    def _mask(self):
-        v = self.vec
-        m = ((v.eff.unsqueeze(-1) >> self._bits) & 1).reshape(self.num_envs, -1)[:, :v.num_actions]
-        return m.bool()
-
-    def _reset_where(self, m: torch.Tensor):
-        v = self.vec
-        mm = m.to(torch.uint8).contiguous()
-        v.ctx.reset(v.num_envs, v.board.data_ptr(), v.rng.data_ptr(), v.timer.data_ptr(), v.eff.data_ptr(),
-                    mm.data_ptr(), v._stream())
+        return {"board": self._board(self.vec.board), "num_moves_left": self._c(self._left)}
 
     # -------------------------------------------------------------------- API
     def reset(self, seed=None, options=None):
         """Reset every env; `seed` (int) re-seeds env i with seed + i (list: one seed per env)."""
+        v = self.vec
         if seed is not None:
             seeds = list(seed) if isinstance(seed, (list, tuple, np.ndarray)) else range(int(seed), int(seed) + self.num_envs)
-            self.vec.set_seed(seeds)
-        self.vec.reset()
-        self._autoreset.zero_()
+            v.set_seed(seeds)
+        v.reset()
+        self._term.zero_()
+        self._left.fill_(self.num_moves)
         infos = {}
-        if self.action_masks:
-            infos["action_mask"] = self._mask()
+        if self.action_masks:          # the step kernels keep it up to date from here on
+            m = ((v.eff.unsqueeze(-1) >> self._bits) & 1).reshape(self.num_envs, -1)[:, :v.num_actions]
+            self._mask.copy_(m)
+            infos["action_mask"] = self._c(self._mask.view(torch.bool))
         return self._obs(), infos
+
+    def stagger_phases(self, **kw):
+        """TileMatchVecEnv.stagger_phases on the envs (episode phases offset by
+        timers, e.g. for benchmarking), with moves left updated."""
+        self.vec.stagger_phases(**kw)
+        self._left.copy_(self.num_moves - self.vec.timer.to(torch.int64))
 
     def step(self, actions):
         v = self.vec
-        a = torch.as_tensor(actions, device=self.device).to(torch.int32).contiguous()
+        a = actions if isinstance(actions, torch.Tensor) else torch.as_tensor(actions)
+        if a.device != self.device or a.dtype != torch.int32:
+            a = a.to(device=self.device, dtype=torch.int32)
+        a = a.contiguous()
         if a.shape != (self.num_envs,):
             raise ValueError(f"actions must have shape ({self.num_envs},)")
-        prev_reset = self._autoreset.clone()
-        v.step_raw(a)                      # envs that ended last step: FLAG_ERROR, state untouched
-        flags = v.flags
-        term = (flags & _native.FLAG_DONE) != 0
+        v.step_raw(a)                      # next step: the envs that ended last call are reset in the kernel
+        v.join()
+        tb = self._term.view(torch.bool)
         infos = {}
-        if self.autoreset_mode == "next_step":
-            self._reset_where(prev_reset)
-            term = term & ~prev_reset
-            rewards = torch.where(prev_reset, torch.zeros_like(v.reward), v.reward)
-            self._autoreset = term.clone()
-        else:
-            rewards = v.reward.clone()
-            if self.obs_dtype == torch.int8:
-                final_board = v.board.clone()
-            else:
-                final_board = v.board.to(torch.int32)
-            infos["final_obs"] = {"board": final_board,
-                                  "num_moves_left": (self.num_moves - v.timer).to(torch.int64)}
-            infos["_final_obs"] = term.clone()
-            self._reset_where(term)
-        live = ~prev_reset if self.autoreset_mode == "next_step" else torch.ones_like(term)
-        zero_i = torch.zeros_like(v.n_new)
-        infos["is_combination_match"] = ((flags & _native.FLAG_COMBO) != 0) & live
-        infos["num_new_specials"] = torch.where(live, v.n_new, zero_i)
-        infos["num_specials_activated"] = torch.where(live, v.n_act, zero_i)
-        infos["shuffled"] = ((flags & _native.FLAG_SHUFFLED) != 0) & live
-        # a live env whose step met an internal error / capacity overflow (never expected)
-        infos["error"] = ((flags & (_native.FLAG_ERROR | _native.FLAG_OVERFLOW)) != 0) & live
+        if self.autoreset_mode == "same_step":
+            infos["final_obs"] = {"board": self._board(self._final), "num_moves_left": self._zero_left}
+            infos["_final_obs"] = self._c(tb[:, 0])
+        infos["is_combination_match"] = self._c(tb[:, 1])
+        infos["num_new_specials"] = self._c(v.n_new)
+        infos["num_specials_activated"] = self._c(v.n_act)
+        infos["shuffled"] = self._c(tb[:, 2])
+        # a live env whose step met an internal error (never expected)
+        infos["error"] = self._c(tb[:, 3])
         if self.action_masks:
-            infos["action_mask"] = self._mask()
-        trunc = torch.zeros_like(term)
-        return self._obs(), rewards, term, trunc, infos
+            infos["action_mask"] = self._c(self._mask.view(torch.bool))
+        return self._obs(), self._c(v.reward), self._c(tb[:, 0]), self._trunc, infos
 
     def close(self):
         self.vec.close()

@@ -3,8 +3,12 @@ wave-instructions per env-step for bench.py's `roofline.issue`.
 
     python tools/issue.py gpurun_out/issue STEPS_PLUS_WARMUP > profiles/issue.json
 
-Each `<cfg>` directory holds one `--pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_WAVES
-...` pass of `bench.py --config <cfg> --steps S --warmup W --no-cpu-baseline`.
+Each `<run>` directory holds one `--pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_WAVES
+...` pass of `bench.py <run's args> --steps S --warmup W --no-cpu-baseline`
+(bench.run_args: a config, c4 = the c2 shard of 131 072 boards, `-eff` = the
+effective-action policy), and `<run>.log` that run's bench line, whose build
+hash, policy, boards and env groups are recorded with the counts (bench.py
+attaches a profile only to a line of the same build and run shape).
 Counted: every step_kernel dispatch and every reset_kernel dispatch issued
 after the first step_kernel one (the deferred autoreset launches of the
 512-cell / general kernels are part of a step); the initial reset() launch is
@@ -40,9 +44,11 @@ def main():
     root, steps = sys.argv[1], int(sys.argv[2])
     out = {}
     for d in sorted(glob.glob(os.path.join(root, "c*"))):
-        name = os.path.basename(d)                          # a config or a bench.PROFILE_RUNS name
-        cfg, run_boards = bench.PROFILE_RUNS.get(name, (name, 0))
-        if cfg not in bench.CONFIGS or not os.path.isdir(d):
+        name = os.path.basename(d)                          # a bench.run_args name
+        if not os.path.isdir(d):
+            continue
+        line = bench.last_bench_line(d + ".log")
+        if line is None:
             continue
         names, rows = per_dispatch(d)
         order = sorted(names)
@@ -61,7 +67,7 @@ def main():
                 continue
             for c, v in rows[i].items():
                 tot[c] += v
-        boards = run_boards or bench.CONFIGS[cfg][5]           # bench --boards of the profiled run
+        boards = line["config"]["boards_per_gpu"]
         env_steps = steps * boards
         out[name] = {
             "valu_per_env_step": round(tot["SQ_INSTS_VALU"] / env_steps, 2),
@@ -70,13 +76,12 @@ def main():
             "smem_per_env_step": round(tot["SQ_INSTS_SMEM"] / env_steps, 2),
             "waves_per_env_step": round(tot["SQ_WAVES"] / env_steps, 4),
             "env_steps": env_steps,
-            # the bench run these counts belong to (bench.py attaches them only to a line of the same run shape)
-            "boards_per_gpu": boards,
-            "env_groups_per_gpu": 3,
+            # the bench run these counts belong to (bench.py attaches them only to a line of the same build and
+            # run shape)
+            **bench.run_identity(line),
             "dispatches": {"step_kernel": n_step, "reset_kernel": n_reset},
-            "source": (f"rocprofv3 --pmc {' '.join(COUNTERS)} --kernel-trace, bench.py --config {cfg} "
-                       + (f"--boards {boards} " if run_boards else "")
-                       + f"(steps + warmup = {steps}); scripts/gpu_issue.sh, tools/issue.py"),
+            "source": (f"rocprofv3 --pmc {' '.join(COUNTERS)} --kernel-trace, bench.py {' '.join(bench.run_args(name))} "
+                       f"(steps + warmup = {steps}); scripts/gpu_issue.sh, tools/issue.py"),
         }
     json.dump(out, sys.stdout, indent=1)
     print()

@@ -40,11 +40,13 @@ def main():
     import bench
     root = sys.argv[1]
     steps = int(sys.argv[2]) if len(sys.argv) > 2 else None
-    groups = 3                                           # bench's default --groups
     out = {}
     for d in sorted(glob.glob(os.path.join(root, "*_FETCH_SIZE"))):
-        name = os.path.basename(d).split("_")[0]         # a config or a bench.PROFILE_RUNS name
-        cfg, boards = bench.PROFILE_RUNS.get(name, (name, 0))
+        name = os.path.basename(d).split("_")[0]         # a bench.run_args name
+        line = bench.last_bench_line(d + ".log")
+        if line is None or not os.path.isdir(d):
+            continue
+        boards = line["config"]["boards_per_gpu"]
         f = per_dispatch(d, "FETCH_SIZE")
         w = per_dispatch(os.path.join(root, f"{name}_WRITE_SIZE"), "WRITE_SIZE")
         if not f or not w:
@@ -59,11 +61,11 @@ def main():
             "hbm_bytes_per_env_step": (round((2 * sum(per_dispatch(d, "FETCH_SIZE", True))
                                                + sum(per_dispatch(os.path.join(root, f"{name}_WRITE_SIZE"),
                                                                   "WRITE_SIZE", True))) * 1024
-                                              / (steps * (boards or bench.CONFIGS[cfg][5])), 1) if steps else None),
+                                              / (steps * boards), 1) if steps else None),
             "correction": "FETCH_SIZE x2 (gfx950 half-count, MI355X_MICROARCH.md HBM section); WRITE_SIZE as is",
-            # the bench run these counts belong to (bench.py attaches them only to a line of the same run shape)
-            "boards_per_gpu": boards or bench.CONFIGS[cfg][5],
-            "env_groups_per_gpu": groups,
+            # the bench run these counts belong to (bench.py attaches them only to a line of the same build and
+            # run shape)
+            **bench.run_identity(line),
         }
     json.dump(out, sys.stdout, indent=1)
     print()

@@ -314,21 +314,31 @@ static void emu_do_reset(const tmg::Params &P, int64_t n, int8_t *board, uint64_
 
 extern "C" {
 
+// autoreset as tmg_plan_config (0 none, 1 same step, 2 next step); policy /
+// key / first_env / t and the vector-env outputs as tmg_plan_config (NULL: none)
 int emu_step(int R, int C, int k, int smask, int moves, int64_t n, int8_t *board, uint64_t *rng, int32_t *timer,
-             const int32_t *actions, int32_t *reward, int32_t *n_new, int32_t *n_act, uint8_t *flags, uint64_t *eff,
-             int trust_eff, int autoreset) {
+             int32_t *actions, int32_t *reward, int32_t *n_new, int32_t *n_act, uint8_t *flags, uint64_t *eff,
+             int trust_eff, int autoreset, int policy, uint64_t key, int64_t first_env, int32_t t, uint8_t *term,
+             uint8_t *mask, int64_t *left, int8_t *final_board) {
     if (!g_jump_init) { tmg::build_jump_table(g_jump); g_jump_init = true; }
     tmg::Params P = make_params(R, C, k, smask, moves, g_jump);
     P.spill = spill_queue(g_spill_buf, n);
+    P.sample = policy ? 1 : 0;
+    P.pol_key = key;
+    P.pol_first = first_env;
+    P.pol_t = t;
+    P.vo_term = term;
+    P.vo_mask = mask;
+    P.vo_left = left;
+    P.vo_final = final_board;
     EmuStep S;
     S.P = &P; S.n = n; S.board = board; S.rng = rng; S.timer = timer; S.actions = actions; S.reward = reward;
     S.n_new = n_new; S.n_act = n_act; S.flags = flags; S.eff = eff; S.trust_eff = trust_eff; S.autoreset = autoreset;
     const bool lean = smask == 0 && trust_eff;
-    S.autoreset = autoreset ? 1 : 0;
     // as tmg_capi.hip's do_step: the general and 512-cell kernels leave
     // finished boards to a reset launch masked by FL_RESET
-    const int deferred = S.autoreset && (P.N > 128 || !lean);
-    if (deferred) S.autoreset = 2;
+    const int deferred = autoreset && (P.N > 128 || !lean);
+    S.autoreset = autoreset == 0 ? 0 : autoreset == 1 ? (deferred ? 2 : 1) : (deferred ? 4 : 3);
     if (P.N <= 128) {
         if (lean) {
             if (sb_ok(P) && emu_is_shape<tmg::kFixC2>(P)) emu_step_kernel<128, false, 2, false, tmg::kFixC2>(S);
