@@ -278,6 +278,10 @@ bool shape_viable(int R, int C, int k) {
                 for (int v = kk - 1; v > 0; v--) std::swap(order[p * 16 + v], order[p * 16 + rnd() % (v + 1)]);
             }
         }
+        // backtracked past the first cell: every line-free board was tried
+        // (none playable), so the shape is not viable; only a search cut off
+        // by the 4096-board cap restarts with another colour order
+        if (p < 0 && complete <= 4096) return false;
     }
     return false;
 }

@@ -80,7 +80,7 @@ class TileMatchVecEnv:
         self.colourless_specials = list(colourless_specials)
         self.colour_specials = list(colour_specials)
         self.specials_mask = _native.specials_mask(colourless_specials, colour_specials)
-        self.autoreset = bool(autoreset)
+        self._autoreset = bool(autoreset)
         # lib_path: another build of libtmg.so (a diagnostic variant) for this env's context
         self.ctx = _native.Context(device.index if device.index is not None else torch.cuda.current_device(),
                                    num_rows, num_cols, num_colours, self.specials_mask, num_moves, lib_path=lib_path)
@@ -124,6 +124,21 @@ class TileMatchVecEnv:
         self._configure()
 
     # ----------------------------------------------------------------- API
+    @property
+    def autoreset(self) -> bool:
+        """Same-step autoreset of the envs whose episode ends (settable: the step
+        plans are reconfigured)."""
+        return self._autoreset
+
+    @autoreset.setter
+    def autoreset(self, value):
+        value = bool(value)
+        if value != self._autoreset:
+            self._autoreset = value
+            self.join()
+            self._autoreset_mode = "same_step" if value else "none"
+            self._configure()
+
     def _stream(self):
         return _raw_stream(self._dev_index)
 
