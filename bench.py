@@ -218,8 +218,9 @@ def main():
     ap.add_argument("--warmup", type=int, default=30)
     ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
     ap.add_argument("--boards", type=int, default=0, help="override boards per GPU")
-    ap.add_argument("--groups", type=int, default=3,
-                    help="env groups per GPU, each stepped on its own HIP stream (TileMatchVecEnv(groups=))")
+    ap.add_argument("--groups", type=int, default=None,
+                    help="env groups per GPU, each stepped on its own HIP stream (TileMatchVecEnv(groups=)); "
+                         "default 3 (--api vector: 1, its step joins every group each call)")
     ap.add_argument("--policy", default="uniform", choices=("uniform", "effective"),
                     help="uniform: random actions over all A (headline); effective: every env samples uniformly "
                          "from its effective actions on device each step (SURVEY §8(d) secondary mode)")
@@ -241,6 +242,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--dry-run", action="store_true", help="print each rank's shard layout and exit (no GPU)")
     args = ap.parse_args()
+    if args.groups is None:
+        args.groups = 1 if args.api == "vector" else 3
 
     from tile_match_gym_amd.shard import dist_env, max_over_ranks, shard_range, shard_seeds, synthetic_actions
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:

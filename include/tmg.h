@@ -128,7 +128,8 @@ TMG_API int tmg_plan_create(tmg_plan **out, tmg_ctx *ctx, int64_t n, int8_t *boa
  *     is ignored, reward / n_new / n_act / flags 0 but TMG_FLAG_RESET.
  *   policy != 0: actions[] is an output: env i plays a uniform draw over its
  *     effective actions, exactly tmg_sample_effective(key, first_env + i, t)
- *     (src/examples/q_learning.py:19-25), sampled inside the step.
+ *     (src/examples/q_learning.py:19-25), drawn inside the step (the lean
+ *     kernels) or by the sampler kernel enqueued right before it.
  *   onehot / onehot_dtype: fused OneHotWrapper planes, as tmg_step_onehot.
  *   terminated [n][4] bytes: terminated, is_combination_match, shuffled,
  *     error (0/1 each; the reference's step info, tile_match_env.py:102-112).
@@ -139,10 +140,13 @@ TMG_API int tmg_plan_create(tmg_plan **out, tmg_ctx *ctx, int64_t n, int8_t *boa
  *   moves_left [n]: num_moves - timer after the call (tile_match_env.py:114-116).
  *   final_board [n][2][R][C]: with autoreset 1, the board each env whose
  *     episode ended had before its regeneration (rows of other envs untouched).
+ *   board32 [n][2][R][C] int32: the boards in the reference's observation
+ *     dtype (tile_match_env.py:52-77), kept up to date like action_mask
+ *     (initialise it after a reset).
  * Any output pointer may be NULL (not written). */
 TMG_API int tmg_plan_config(tmg_plan *plan, int autoreset, int policy, uint64_t key, int64_t first_env,
                             void *onehot, int onehot_dtype, uint8_t *terminated, uint8_t *action_mask,
-                            int64_t *moves_left, int8_t *final_board);
+                            int64_t *moves_left, int8_t *final_board, int32_t *board32);
 
 /* One step of every env: the group streams first wait for the work queued
  * on `stream` (an event), then each group's launches are enqueued on its

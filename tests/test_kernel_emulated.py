@@ -242,9 +242,9 @@ def test_plan_vector_outputs_emulated(emu_lib, cfg, mode):
     """tmg_plan_config's Gymnasium vector-env step (include/tmg.h): next-step
     autoreset done by the kernels (inline for the lean kernels, by the masked
     reset launch for the others), and the per-env outputs written in the
-    kernels' write-back — terminated / info bytes, action-mask bytes (kept
-    across steps: rows rewritten only where the mask changes), moves left,
-    same-step final boards — against the oracle driven with the same semantics."""
+    kernels' write-back — terminated / info bytes, action-mask bytes and int32
+    boards (kept across steps: rows rewritten only where they change), moves
+    left, same-step final boards — against the oracle driven with the same semantics."""
     from oracle import oracle as orc
     from tile_match_gym_amd.seeding import batch_rng_words
     from vector_ref import VectorOracle, mask_bytes
@@ -259,7 +259,8 @@ def test_plan_vector_outputs_emulated(emu_lib, cfg, mode):
     o.reset()
     ref = VectorOracle(o, mode)
     outs = {"terminated": np.zeros((n, 4), np.uint8), "action_mask": mask_bytes(e.eff, A),
-            "moves_left": np.full(n, moves, np.int64), "final_board": np.zeros((n, 2, R, C), np.int8)}
+            "moves_left": np.full(n, moves, np.int64), "final_board": np.zeros((n, 2, R, C), np.int8),
+            "board32": e.board.astype(np.int32)}
     rs = np.random.default_rng(R + C + k + sm)
     for t in range(3 * moves + 2):
         a = rs.integers(0, A, n).astype(np.int32)
@@ -271,6 +272,7 @@ def test_plan_vector_outputs_emulated(emu_lib, cfg, mode):
             assert np.array_equal(getattr(e, f), want[f]), (cfg, mode, t, f)
         for f in ("terminated", "action_mask", "moves_left"):
             assert np.array_equal(outs[f], want[f]), (cfg, mode, t, f)
+        assert np.array_equal(outs["board32"], o.board.astype(np.int32)), (cfg, mode, t, "board32")
         if mode == "same_step":
             term = want["terminated"][:, 0].astype(bool)
             assert np.array_equal(outs["final_board"][term], want["final_board"][term]), (cfg, t)

@@ -30,7 +30,7 @@ namespace tmg {
 
 // Minimum waves per SIMD asked of the register allocator (launch bounds), per
 // kernel; each measured on the MI355X against its neighbours.
-constexpr int kLean128Waves = 7;     // step_kernel<128, false>: the c2 / c4 kernel (72 VGPRs)
+constexpr int kLean128Waves = 7;     // step_kernel<128, false>: the c2 / c4 kernel (72 VGPRs; 8: 64, 1 % slower)
 constexpr int kGen128Waves = 5;      // step_kernel<128, true>: c3 (96 VGPRs; 6 / 7 spill and lose, also specialised)
 constexpr int kReset512Waves = 8;    // reset_kernel<512>: c5's regeneration (7: 0.8 % slower, profiles/r04/s7)
 constexpr int kReset128Waves = 8;    // reset_kernel<128> specialised for 10x10 k4 (c3): 63 VGPRs
@@ -161,6 +161,8 @@ struct Params {
     int64_t *vo_left;             // [n]: num_moves_left after the call (tile_match_env.py:114-116)
     int8_t *vo_final;             // [n][2][R][C]: same-step autoreset, the last board of each env whose
                                   // episode ended, before its regeneration
+    int32_t *vo_obs;              // [n][2][R][C]: the board as int32 (the reference's observation dtype),
+                                  // rewritten where the board changes
     // in-kernel policy (tmg_step_groups with a policy key): actions[e] <- uniform
     // over env e's effective actions, the stream of tmg_sample_effective
     int sample;
@@ -219,6 +221,7 @@ inline Params make_params(int R, int C, int k, int smask, int num_moves, const u
     P.vo_mask = nullptr;
     P.vo_left = nullptr;
     P.vo_final = nullptr;
+    P.vo_obs = nullptr;
     P.sample = 0;
     P.pol_t = 0;
     P.pol_first = 0;
@@ -600,6 +603,13 @@ __device__ __forceinline__ void store_mask(const Params &P, const WS &w, int lan
     } else {
         for (int i = lane; i < A; i += 64) m[i] = zero ? (uint8_t)0 : (uint8_t)((w.effw[i >> 6] >> (i & 63)) & 1ULL);
     }
+}
+
+// The board of env e in LDS as the int32 observation (Params::vo_obs)
+template <class WS>
+__device__ __forceinline__ void store_obs(const Params &P, const WS &w, int lane, int64_t e) {
+    int32_t *o = P.vo_obs + e * 2 * (int64_t)P.N;
+    for (int p = lane; p < 2 * P.N; p += 64) o[p] = w.brd[p];
 }
 
 // Per-env outputs of tmg_step_groups besides the step's own (lane 0)
@@ -2305,6 +2315,25 @@ __device__ __forceinline__ uint32_t step_env(
     // state there too measured slower: the quick waves wait for those loads.
     const uint64_t effrow = lane < W ? eff[e * W + lane] : 0ULL;
     TMG_KEEP_V(effrow);
+    // The effective path's loads issued together, before anything waits on
+    // one: the board (when whole dwords), the RNG state and this lane's
+    // jump-table row.  One memory round trip instead of three dependent ones
+    // (board -> LDS -> precondition -> RNG -> jump table).  With the in-kernel
+    // policy every move is effective, so they go out with the mask row;
+    // otherwise after the ineffective-move exit.
+    int8_t *gb = board + e * 2 * N;
+    const int nbw = (2 * N) >> 2;
+    const bool bwhole = ((2 * N) & 3) == 0 && nbw <= 64;
+    uint32_t bw = 0;
+    uint64_t q0 = 0, q1 = 0, q2 = 0, q3 = 0, q4 = 0, j0 = 0, j1 = 0, j2 = 0, j3 = 0;
+    const auto issue_loads = [&]() {
+        bw = bwhole ? reinterpret_cast<const uint32_t *>(gb)[lane < nbw ? lane : 0] : 0u;
+        const uint64_t *rp = rng + e * 5;
+        q0 = rp[0]; q1 = rp[1]; q2 = rp[2]; q3 = rp[3]; q4 = rp[4];
+        const uint64_t *jt = P.jump + lane * 4;
+        j0 = jt[0]; j1 = jt[1]; j2 = jt[2]; j3 = jt[3];
+    };
+    if (P.sample) issue_loads();
     if (P.sample) {                                                         // the policy's action, from the mask
         a = __builtin_amdgcn_readfirstlane(sample_action(P, effrow, e));
         if (lane == 0) const_cast<int32_t *>(actions)[e] = a;
@@ -2315,14 +2344,14 @@ __device__ __forceinline__ uint32_t step_env(
             reward[e] = 0; n_new[e] = 0; n_act[e] = 0; flags_out[e] = FL_ERR;
             store_vo(P, e, FL_ERR, t0);
         }
-        if (P.oh && !trust_eff) {             // the fused planes follow every board of an untrusted call
+        if ((P.oh || P.vo_obs) && !trust_eff) {   // the fused outputs follow every board of an untrusted call
             load_board(P, w, lane, board + e * 2 * N);
             WSYNC();
-            store_onehot(P, w, lane, e);
+            if (P.oh) store_onehot(P, w, lane, e);
+            if (P.vo_obs) store_obs(P, w, lane, e);
         }
         return ST_CALLER;
     }
-    int8_t *gb = board + e * 2 * N;
     uint64_t *ge = eff + e * W;
     const int t1 = t0 + 1;
     const bool done = !pend && t1 == P.num_moves;                           // tile_match_env.py:100-101
@@ -2340,7 +2369,6 @@ __device__ __forceinline__ uint32_t step_env(
             if (P.vo_mask) store_mask(P, w, lane, e, true);
         }
         if (done && same && P.vo_final) {                                   // the last board, as it stands
-            const int nbw = (2 * N) >> 2;
             const uint32_t *src = reinterpret_cast<const uint32_t *>(gb);
             uint32_t *dst = reinterpret_cast<uint32_t *>(P.vo_final + e * 2 * N);
             for (int i = lane; i < nbw; i += 64) dst[i] = src[i];
@@ -2358,17 +2386,7 @@ __device__ __forceinline__ uint32_t step_env(
     action_coords(P.R, P.C, a, r1, c1, r2, c2);
     const int p1 = r1 * P.C + c1, p2 = r2 * P.C + c2;
 
-    // The effective path's loads issued together, before anything waits on
-    // one: the board (when whole dwords), the RNG state and this lane's
-    // jump-table row.  One memory round trip instead of three dependent ones
-    // (board -> LDS -> precondition -> RNG -> jump table).
-    const int nbw = (2 * N) >> 2;
-    const bool bwhole = ((2 * N) & 3) == 0 && nbw <= 64;
-    const uint32_t bw = bwhole ? reinterpret_cast<const uint32_t *>(gb)[lane < nbw ? lane : 0] : 0u;
-    const uint64_t *rp = rng + e * 5;
-    const uint64_t q0 = rp[0], q1 = rp[1], q2 = rp[2], q3 = rp[3], q4 = rp[4];
-    const uint64_t *jt = P.jump + lane * 4;
-    const uint64_t j0 = jt[0], j1 = jt[1], j2 = jt[2], j3 = jt[3];
+    if (!P.sample) issue_loads();
     if (bwhole) {
         if (lane < nbw) reinterpret_cast<uint32_t *>(w.brd)[lane] = bw;
     } else {
@@ -2449,6 +2467,7 @@ __device__ __forceinline__ uint32_t step_env(
     // fused one-hot planes: every board this step changed (or, with an
     // untrusted mask, any board: it may have been edited by hand)
     if (P.oh && (changed || !trust_eff)) store_onehot(P, w, lane, e);
+    if (P.vo_obs && (changed || !trust_eff)) store_obs(P, w, lane, e);
     if (done && !same) {
         for (int i = lane; i < W; i += 64) ge[i] = 0ULL;                   // tile_match_env.py:119-120
         if (P.vo_mask) store_mask(P, w, lane, e, true);
@@ -2622,6 +2641,7 @@ __device__ __forceinline__ void reset_env(const Params &P, WS &w, int lane, int6
     store_board(P, w, lane, board + e * 2 * N);
     store_rng(rng + e * 5, g, lane);
     if (P.oh) store_onehot(P, w, lane, e);
+    if (P.vo_obs) store_obs(P, w, lane, e);
     for (int i = lane; i < W; i += 64) eff[e * W + i] = w.effw[i];
     if (P.vo_mask) store_mask(P, w, lane, e, false);
     if (lane == 0) {

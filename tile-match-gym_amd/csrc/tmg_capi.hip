@@ -532,7 +532,7 @@ int tmg_plan_create(tmg_plan **out, tmg_ctx *ctx, int64_t n, int8_t *board, uint
 
 int tmg_plan_config(tmg_plan *p, int autoreset, int policy, uint64_t key, int64_t first_env, void *onehot,
                     int onehot_dtype, uint8_t *terminated, uint8_t *action_mask, int64_t *moves_left,
-                    int8_t *final_board) {
+                    int8_t *final_board, int32_t *board32) {
     if (!p) return fail(-1, "null plan");
     if (autoreset < 0 || autoreset > 2) return fail(-2, "autoreset must be 0 (none), 1 (same step) or 2 (next step)");
     if (first_env < 0) return fail(-2, "first_env must be >= 0");
@@ -543,6 +543,7 @@ int tmg_plan_config(tmg_plan *p, int autoreset, int policy, uint64_t key, int64_
     P.vo_mask = action_mask;
     P.vo_left = moves_left;
     P.vo_final = final_board;
+    P.vo_obs = board32;
     P.sample = policy ? 1 : 0;
     P.pol_key = key;
     p->P = P;
@@ -581,11 +582,22 @@ int tmg_plan_step(tmg_plan *p, int32_t *actions, int32_t t, int trust_eff, void 
         if (P.vo_mask) P.vo_mask += lo * A;
         if (P.vo_left) P.vo_left += lo;
         if (P.vo_final) P.vo_final += lo * 2 * N;
+        if (P.vo_obs) P.vo_obs += lo * 2 * N;
         P.pol_first = p->first_env + lo;
         P.pol_t = t;
+        const hipStream_t gs = p->streams[g] ? p->streams[g] : cur;
+        if (P.sample && !(ctx->P.smask == 0 && trust_eff)) {
+            // the general kernels (low occupancy, long waves) take the draw
+            // from the sampler kernel ahead of them; the lean ones sample in
+            // their own prologue
+            tmg::launch_sample_effective(gs, m, W, A, p->eff + lo * W, p->key, p->first_env + lo, t, actions + lo);
+            rc = hip_check(hipGetLastError(), "kernel launch");
+            if (rc) return rc;
+            P.sample = 0;
+        }
         const StepArgs a{m, p->board + lo * 2 * N, p->rng + lo * 5, p->timer + lo, actions + lo, p->reward + lo,
                          p->n_new + lo, p->n_act + lo, p->flags + lo, p->eff + lo * W, trust_eff, p->autoreset};
-        rc = do_step(ctx, P, a, p->streams[g] ? p->streams[g] : cur);
+        rc = do_step(ctx, P, a, gs);
         if (rc) return rc;
     }
     return 0;

@@ -85,7 +85,7 @@ def load(path: str = None):
     L.tmg_step_onehot.argtypes = [P, I64, P, P, P, P, P, P, P, P, P, I, I, P, I, P]
     L.tmg_reset_onehot.argtypes = [P, I64, P, P, P, P, P, P, I, P]
     L.tmg_plan_create.argtypes = [ctypes.POINTER(P), P, I64, P, P, P, P, P, P, P, P, I, P, P]
-    L.tmg_plan_config.argtypes = [P, I, I, ctypes.c_uint64, I64, P, I, P, P, P, P]
+    L.tmg_plan_config.argtypes = [P, I, I, ctypes.c_uint64, I64, P, I, P, P, P, P, P]
     L.tmg_plan_step.argtypes = [P, P, ctypes.c_int32, I, P]
     L.tmg_plan_join.argtypes = [P, P]
     L.tmg_plan_destroy.argtypes = [P]
@@ -253,10 +253,10 @@ class Plan:
         self._join = L.tmg_plan_join
 
     def config(self, autoreset="same_step", policy=False, key=0, first_env=0, onehot=None, onehot_dtype=DTYPE_F32,
-               terminated=None, action_mask=None, moves_left=None, final_board=None):
+               terminated=None, action_mask=None, moves_left=None, final_board=None, board32=None):
         check(self._L.tmg_plan_config(self._h, self.AUTORESET[autoreset], int(bool(policy)),
                                       int(key) & 0xFFFFFFFFFFFFFFFF, int(first_env), onehot, int(onehot_dtype),
-                                      terminated, action_mask, moves_left, final_board), self._L)
+                                      terminated, action_mask, moves_left, final_board, board32), self._L)
 
     def step(self, actions_ptr: int, t: int, trust_eff: int, stream: int):
         rc = self._step(self._h, actions_ptr, t, trust_eff, stream)

@@ -150,19 +150,22 @@ class TileMatchVecEnv:
                         onehot=_ptr(self.onehot), onehot_dtype=self._oh_code, **self._vout)
 
     def set_step_outputs(self, autoreset_mode: str = None, terminated=None, action_mask=None, moves_left=None,
-                         final_board=None):
+                         final_board=None, board32=None):
         """Outputs every step writes in the kernels' own write-back (tmg_plan_config):
         terminated (N, 4) uint8 (terminated, is_combination_match, shuffled, error),
         action_mask (N, A) uint8/bool (kept up to date: rows are rewritten where the
         mask changes, so initialise it after a reset), moves_left (N,) int64,
         final_board (N, 2, R, C) int8 (same-step autoreset: the last board of each
-        env whose episode ended).  autoreset_mode: "none", "same_step", "next_step"."""
+        env whose episode ended), board32 (N, 2, R, C) int32 (the boards in the
+        reference's observation dtype, kept up to date like action_mask).
+        autoreset_mode: "none", "same_step", "next_step"."""
         self.join()
         if autoreset_mode is not None:
             self._autoreset_mode = autoreset_mode
         self._vout = {k: _ptr(v) for k, v in (("terminated", terminated), ("action_mask", action_mask),
-                                               ("moves_left", moves_left), ("final_board", final_board))}
-        self._vout_refs = (terminated, action_mask, moves_left, final_board)
+                                               ("moves_left", moves_left), ("final_board", final_board),
+                                               ("board32", board32))}
+        self._vout_refs = (terminated, action_mask, moves_left, final_board, board32)
         self._configure()
 
     def set_seed(self, seeds):

@@ -27,7 +27,8 @@ batching follows gymnasium.vector.VectorEnv:
 One host call per step (a tmg_plan step over the env groups' streams): the
 kernels themselves reset the envs due (next-step mode), keep the (N, A) mask
 bytes of the envs whose mask changed, and write the terminated / info bytes,
-moves left and (same-step mode) the final boards.  The returned tensors are
+moves left, the int32 observation boards and (same-step mode) the final
+boards.  The returned tensors are
 views of the env's live buffers, overwritten by the next call; pass
 ``copy=True`` for fresh tensors (gymnasium's vector-env ``copy`` flag).
 """
@@ -85,11 +86,12 @@ class TileMatchVectorEnv:
         self._left = torch.zeros(num_envs, dtype=torch.int64, **kw)
         self._final = (torch.zeros((num_envs, 2, R, C), dtype=torch.int8, **kw)
                        if autoreset_mode == "same_step" else None)
+        self._obs32 = torch.zeros((num_envs, 2, R, C), dtype=torch.int32, **kw) if obs_dtype == torch.int32 else None
         self._trunc = torch.zeros(num_envs, dtype=torch.bool, **kw)
         self._zero_left = torch.zeros(num_envs, dtype=torch.int64, **kw)
         self._bits = torch.arange(64, device=self.device, dtype=torch.int64)
         self.vec.set_step_outputs(autoreset_mode, terminated=self._term, action_mask=self._mask,
-                                  moves_left=self._left, final_board=self._final)
+                                  moves_left=self._left, final_board=self._final, board32=self._obs32)
 
     # ---------------------------------------------------------------- helpers
     def _c(self, t):
@@ -99,7 +101,8 @@ class TileMatchVectorEnv:
         return self._c(b) if self.obs_dtype == torch.int8 else b.to(torch.int32)
 
     def _obs(self):
-        return {"board": self._board(self.vec.board), "num_moves_left": self._c(self._left)}
+        b = self._obs32 if self._obs32 is not None else self.vec.board       # int32: kept by the kernels
+        return {"board": self._c(b), "num_moves_left": self._c(self._left)}
 
     # -------------------------------------------------------------------- API
     def reset(self, seed=None, options=None):
@@ -109,6 +112,8 @@ class TileMatchVectorEnv:
             seeds = list(seed) if isinstance(seed, (list, tuple, np.ndarray)) else range(int(seed), int(seed) + self.num_envs)
             v.set_seed(seeds)
         v.reset()
+        if self._obs32 is not None:        # the step kernels keep it up to date from here on
+            self._obs32.copy_(v.board)
         self._term.zero_()
         self._left.fill_(self.num_moves)
         infos = {}

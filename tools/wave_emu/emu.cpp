@@ -319,7 +319,7 @@ extern "C" {
 int emu_step(int R, int C, int k, int smask, int moves, int64_t n, int8_t *board, uint64_t *rng, int32_t *timer,
              int32_t *actions, int32_t *reward, int32_t *n_new, int32_t *n_act, uint8_t *flags, uint64_t *eff,
              int trust_eff, int autoreset, int policy, uint64_t key, int64_t first_env, int32_t t, uint8_t *term,
-             uint8_t *mask, int64_t *left, int8_t *final_board) {
+             uint8_t *mask, int64_t *left, int8_t *final_board, int32_t *board32) {
     if (!g_jump_init) { tmg::build_jump_table(g_jump); g_jump_init = true; }
     tmg::Params P = make_params(R, C, k, smask, moves, g_jump);
     P.spill = spill_queue(g_spill_buf, n);
@@ -331,6 +331,7 @@ int emu_step(int R, int C, int k, int smask, int moves, int64_t n, int8_t *board
     P.vo_mask = mask;
     P.vo_left = left;
     P.vo_final = final_board;
+    P.vo_obs = board32;
     EmuStep S;
     S.P = &P; S.n = n; S.board = board; S.rng = rng; S.timer = timer; S.actions = actions; S.reward = reward;
     S.n_new = n_new; S.n_act = n_act; S.flags = flags; S.eff = eff; S.trust_eff = trust_eff; S.autoreset = autoreset;

@@ -19,7 +19,7 @@ I64 = ctypes.c_int64
 def load(asan=False):
     L = ctypes.CDLL(os.path.join(HERE, "libwave_emu_asan.so" if asan else os.environ.get("EMU_LIB", "libwave_emu.so")))
     L.emu_step.argtypes = [I, I, I, I, I, I64, P, P, P, P, P, P, P, P, P, I, I, I, ctypes.c_uint64, I64, ctypes.c_int32,
-                           P, P, P, P]
+                           P, P, P, P, P]
     L.emu_reset.argtypes = [I, I, I, I, I, I64, P, P, P, P]
     L.emu_reset_masked.argtypes = [I, I, I, I, I, I64, P, P, P, P, P, I]
     L.emu_effective.argtypes = [I, I, I, I, I64, P, P]
@@ -72,7 +72,7 @@ class EmuBatch:
         """mode: 0 none / 1 same step / 2 next step (tmg_plan_config; default from
         autoreset); policy = (key, first_env, t): actions is then the output
         array of the in-kernel draw; outputs: dict of numpy arrays terminated
-        (n, 4) u8, action_mask (n, A) u8, moves_left (n,) i64, final_board."""
+        (n, 4) u8, action_mask (n, A) u8, moves_left (n,) i64, final_board, board32."""
         a = actions if policy is not None else np.ascontiguousarray(actions, dtype=np.int32)
         mode = (1 if autoreset else 0) if mode is None else mode
         key, first, t = policy if policy is not None else (0, 0, 0)
@@ -82,7 +82,8 @@ class EmuBatch:
                         self.rng.ctypes.data, self.timer.ctypes.data, a.ctypes.data, self.reward.ctypes.data,
                         self.n_new.ctypes.data, self.n_act.ctypes.data, self.flags.ctypes.data,
                         self.eff.ctypes.data, int(self.trust), int(mode), int(policy is not None), int(key), int(first),
-                        int(t), ptr("terminated"), ptr("action_mask"), ptr("moves_left"), ptr("final_board"))
+                        int(t), ptr("terminated"), ptr("action_mask"), ptr("moves_left"), ptr("final_board"),
+                        ptr("board32"))
 
 
 def main():
