@@ -239,6 +239,9 @@ def main():
     ap.add_argument("--obs-dtype", default="int32", choices=("int32", "int8"),
                     help="--api vector: the observation board dtype (int32 = the reference's, a converted copy; int8 = "
                          "a view of the live state)")
+    ap.add_argument("--graph", type=int, default=0,
+                    help="1: the timed steps are captured into one HIP graph beforehand (TileMatchVecEnv.capture_steps: "
+                         "the same launches, one host call for the whole window; --api raw)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--dry-run", action="store_true", help="print each rank's shard layout and exit (no GPU)")
     args = ap.parse_args()
@@ -317,6 +320,11 @@ def main():
     for t in range(args.warmup):
         step(t)
     env.join()
+    graph = None
+    if args.graph and args.api == "raw":            # capture the timed steps (untimed)
+        ts = [args.warmup + i for i in range(args.steps)]
+        graph = (env.capture_steps(ts=ts, policy=True, first_env=rng_.start) if args.policy == "effective" else
+                 env.capture_steps([acts[t % T] for t in ts], ts))
     torch.cuda.synchronize()
 
     # HIP events: on the current stream around the whole step (fork ... join:
@@ -328,11 +336,15 @@ def main():
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     ev[0].record()
-    env.record(ev[2])
-    for i in range(args.steps):
-        step(args.warmup + i)
+    if graph is not None:
+        env.run_graph(graph)
+    else:
+        env.record(ev[2])
+        for i in range(args.steps):
+            step(args.warmup + i)
     host_issue_s = time.perf_counter() - t0          # host time to enqueue the window (launch-rate check)
-    env.record(ev[3])
+    if graph is None:
+        env.record(ev[3])
     env.join()
     ev[1].record()
     torch.cuda.synchronize()
@@ -340,7 +352,18 @@ def main():
         dist.barrier()
     el = time.perf_counter() - t0
     step_ms = ev[0].elapsed_time(ev[1]) / max(1, args.steps)
-    kern_ms = ev[2].elapsed_time(ev[3]) / max(1, args.steps)
+    if graph is not None:
+        # the graph's kernels run on the runtime's streams: group 0's launch
+        # time from 10 eager steps after the timed window (untimed)
+        env.record(ev[2])
+        for i in range(10):
+            step(args.warmup + args.steps + i)
+        env.record(ev[3])
+        env.join()
+        torch.cuda.synchronize()
+        kern_ms = ev[2].elapsed_time(ev[3]) / 10
+    else:
+        kern_ms = ev[2].elapsed_time(ev[3]) / max(1, args.steps)
     launch_envs = env._ranges[0][1] - env._ranges[0][0]
     st = env.status()                     # sticky: every env of every step, warmup included
     if st & 0x3:
@@ -410,7 +433,7 @@ def main():
                                       f"{args.obs_dtype} obs)"),
                        "boards_per_gpu": nb, "rows": R, "cols": C, "colours": k,
                        "specials": cl + co, "env_groups_per_gpu": env.groups, "policy": args.policy,
-                       "api": args.api,
+                       "api": args.api, "graph": bool(graph is not None),
                        "parallelism": f"dp{world} (independent env shards, no collective)"},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 6),

@@ -160,6 +160,19 @@ TMG_API int tmg_plan_step(tmg_plan *plan, int32_t *actions, int32_t t, int trust
 TMG_API int tmg_plan_join(tmg_plan *plan, void *stream);
 TMG_API int tmg_plan_destroy(tmg_plan *plan);
 
+/* `steps` consecutive tmg_plan_step calls (step k: actions[k], t[k]; trust_eff
+ * for the first, 1 after it) and the final tmg_plan_join, captured on
+ * `stream` (a created stream, not NULL) into a HIP graph: tmg_graph_launch
+ * then enqueues all of them on a stream with one call, the env groups'
+ * launches still overlapping across the steps inside it.  Nothing runs at
+ * capture time.  The graph keeps the plan's buffers, the action pointers and
+ * the configuration of the moment; re-capture after tmg_plan_config. */
+typedef struct tmg_graph tmg_graph;
+TMG_API int tmg_plan_capture(tmg_plan *plan, int steps, int32_t *const *actions, const int32_t *t, int trust_eff,
+                             void *stream, tmg_graph **out);
+TMG_API int tmg_graph_launch(tmg_graph *graph, void *stream);
+TMG_API int tmg_graph_destroy(tmg_graph *graph);
+
 /* Replaces TileMatchEnv._get_effective_actions (tile_match_env.py:118-124,
  * is_move_effective board.py:735-787) as a bitmask, ignoring the timer. */
 TMG_API int tmg_effective(tmg_ctx *ctx, int64_t n, const int8_t *board, uint64_t *eff, void *stream);

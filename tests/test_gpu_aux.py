@@ -279,3 +279,37 @@ def test_step_effective_after_hand_edit_with_low_line(R, C, k, sm):
         assert np.array_equal(env.rng_words(), o.rng), t
         assert np.array_equal(env.eff.cpu().numpy().view(np.uint64), o.eff), t
     assert env.status() == 0
+
+
+@pytest.mark.parametrize("cfg", [(10, 10, 4, 0), (8, 8, 3, 14)])
+@pytest.mark.parametrize("policy", [False, True])
+def test_captured_steps_match_eager(cfg, policy):
+    """TileMatchVecEnv.capture_steps / run_graph (tmg_plan_capture: the plan
+    steps of a window in one HIP graph) leaves exactly the state of the same
+    steps launched one by one: lean and general kernels, three env groups,
+    given actions and the in-kernel policy, across autoresets."""
+    from tile_match_gym_amd.shard import synthetic_actions
+    from tile_match_gym_amd.vec_env import TileMatchVecEnv
+    R, C, k, sm = cfg
+    n, T = 3000, 24
+    cl, co = _lists(sm)
+    envs = [TileMatchVecEnv(n, R, C, k, 7, cl, co, seed=3, device=DEV, groups=3) for _ in range(2)]
+    A = envs[0].num_actions
+    acts = torch.from_numpy(synthetic_actions(range(n), T, A)).to(DEV)
+    for e in envs:
+        e.reset()
+    for t in range(T):
+        if policy:
+            envs[0].step_effective(t)
+        else:
+            envs[0].step_raw(acts[t])
+    envs[0].join()
+    g = (envs[1].capture_steps(ts=range(T), policy=True) if policy else
+         envs[1].capture_steps([acts[t] for t in range(T)]))
+    envs[1].run_graph(g)
+    torch.cuda.synchronize()
+    for f in ("board", "rng", "timer", "eff", "reward", "n_new", "n_act", "flags"):
+        assert torch.equal(getattr(envs[0], f), getattr(envs[1], f)), (cfg, policy, f)
+    if policy:
+        assert torch.equal(envs[0].actions, envs[1].actions)
+    assert envs[1].status() == 0

@@ -616,6 +616,66 @@ int tmg_plan_join(tmg_plan *p, void *stream) {
     return rc;
 }
 
+// ---------------------------------------------------------- step graphs
+struct tmg_graph {
+    int device;
+    hipGraph_t graph;
+    hipGraphExec_t exec;
+};
+
+int tmg_graph_destroy(tmg_graph *g) {
+    if (!g) return 0;
+    if (g->exec) (void)hipGraphExecDestroy(g->exec);
+    if (g->graph) (void)hipGraphDestroy(g->graph);
+    delete g;
+    return 0;
+}
+
+int tmg_plan_capture(tmg_plan *p, int steps, int32_t *const *actions, const int32_t *t, int trust_eff, void *stream,
+                     tmg_graph **out) {
+    if (!out) return fail(-1, "null output pointer");
+    *out = nullptr;
+    if (!p) return fail(-1, "null plan");
+    if (steps < 1 || !actions || !t) return fail(-2, "a capture needs >= 1 step, its actions and step counters");
+    if (!stream) return fail(-2, "capture on a created stream (the NULL stream cannot be captured)");
+    int rc = set_device(p->ctx);
+    if (rc) return rc;
+    const hipStream_t cur = reinterpret_cast<hipStream_t>(stream);
+    // the general kernels' spill queues must exist before the capture (no
+    // allocation or synchronisation inside it)
+    if (!(p->ctx->P.smask == 0 && trust_eff)) {
+        for (size_t g = 0; g < p->streams.size() && !rc; g++) {
+            tmg::SpillQ *q;
+            void *ws;
+            rc = spill_for(p->ctx, p->streams[g] ? p->streams[g] : cur, p->bounds[g + 1] - p->bounds[g], &q, &ws);
+        }
+        if (rc) return rc;
+    }
+    tmg_graph *gr = new tmg_graph();
+    gr->device = p->ctx->device;
+    rc = hip_check(hipStreamBeginCapture(cur, hipStreamCaptureModeThreadLocal), "hipStreamBeginCapture");
+    if (rc) { delete gr; return rc; }
+    for (int k = 0; k < steps && !rc; k++) rc = tmg_plan_step(p, actions[k], t[k], k ? 1 : trust_eff, stream);
+    if (!rc) rc = tmg_plan_join(p, stream);
+    const int rc_end = hip_check(hipStreamEndCapture(cur, &gr->graph), "hipStreamEndCapture");
+    if (!rc) rc = rc_end;
+    if (!rc) rc = hip_check(hipGraphInstantiate(&gr->exec, gr->graph, nullptr, nullptr, 0), "hipGraphInstantiate");
+    if (rc) { tmg_graph_destroy(gr); return rc; }
+    *out = gr;
+    return 0;
+}
+
+int tmg_graph_launch(tmg_graph *g, void *stream) {
+    if (!g) return fail(-1, "null graph");
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    if (dev != g->device) {
+        int rc = hip_check(hipSetDevice(g->device), "hipSetDevice");
+        if (rc) return rc;
+    }
+    return hip_check(hipGraphLaunch(g->exec, reinterpret_cast<hipStream_t>(stream)), "hipGraphLaunch");
+}
+
 int tmg_plan_destroy(tmg_plan *p) {
     if (!p) return 0;
     if (p->fork) (void)hipEventDestroy(p->fork);

@@ -25,7 +25,8 @@ EXPORTS = ("tmg_create", "tmg_create_scan", "tmg_destroy", "tmg_reset", "tmg_ste
            "tmg_num_actions", "tmg_mask_words", "tmg_last_error", "tmg_abi_version", "tmg_build_info",
            "tmg_onehot", "tmg_onehot_channels", "tmg_count_states", "tmg_sample_effective", "tmg_status",
            "tmg_viable", "tmg_spills", "tmg_step_onehot", "tmg_reset_onehot", "tmg_plan_create", "tmg_plan_config",
-           "tmg_plan_step", "tmg_plan_join", "tmg_plan_destroy")
+           "tmg_plan_step", "tmg_plan_join", "tmg_plan_destroy", "tmg_plan_capture", "tmg_graph_launch",
+           "tmg_graph_destroy")
 DTYPE_F32, DTYPE_U8, DTYPE_I32 = 0, 1, 2
 ABI_VERSION = 4
 STATUS_INTERNAL, STATUS_OVERFLOW, STATUS_CALLER = 1, 2, 4
@@ -89,11 +90,14 @@ def load(path: str = None):
     L.tmg_plan_step.argtypes = [P, P, ctypes.c_int32, I, P]
     L.tmg_plan_join.argtypes = [P, P]
     L.tmg_plan_destroy.argtypes = [P]
+    L.tmg_plan_capture.argtypes = [P, I, P, P, I, P, ctypes.POINTER(P)]
+    L.tmg_graph_launch.argtypes = [P, P]
+    L.tmg_graph_destroy.argtypes = [P]
     for name in ("tmg_create", "tmg_create_scan", "tmg_destroy", "tmg_reset", "tmg_step", "tmg_effective",
                  "tmg_num_actions", "tmg_mask_words", "tmg_abi_version", "tmg_onehot", "tmg_onehot_channels",
                  "tmg_sample_effective", "tmg_status", "tmg_viable", "tmg_spills", "tmg_step_onehot", "tmg_reset_onehot",
                  "tmg_count_states", "tmg_plan_create", "tmg_plan_config", "tmg_plan_step", "tmg_plan_join",
-                 "tmg_plan_destroy"):
+                 "tmg_plan_destroy", "tmg_plan_capture", "tmg_graph_launch", "tmg_graph_destroy"):
         getattr(L, name).restype = I
     if L.tmg_abi_version() != ABI_VERSION:
         raise TmgError("libtmg.so ABI version mismatch; rebuild it")
@@ -268,9 +272,42 @@ class Plan:
         if rc:
             check(rc, self._L)
 
+    def capture(self, actions_ptrs, ts, trust_eff: int, stream: int) -> "StepGraph":
+        """len(actions_ptrs) steps + the join, captured into a HIP graph (tmg_plan_capture)."""
+        k = len(actions_ptrs)
+        a = (P * k)(*[int(x) for x in actions_ptrs])
+        t = (ctypes.c_int32 * k)(*[int(x) for x in ts])
+        h = P()
+        check(self._L.tmg_plan_capture(self._h, k, a, t, int(trust_eff), stream, ctypes.byref(h)), self._L)
+        return StepGraph(self, h, k)
+
     def close(self):
         if getattr(self, "_h", None) is not None and self._h.value:
             self._L.tmg_plan_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class StepGraph:
+    """A captured run of plan steps (tmg_graph): launch() enqueues them all."""
+
+    def __init__(self, plan: Plan, h, steps: int):
+        self._plan, self._h, self.steps = plan, h, steps
+        self._L = plan._L
+
+    def launch(self, stream: int):
+        rc = self._L.tmg_graph_launch(self._h, stream)
+        if rc:
+            check(rc, self._L)
+
+    def close(self):
+        if getattr(self, "_h", None) is not None and self._h.value:
+            self._L.tmg_graph_destroy(self._h)
             self._h = None
 
     def __del__(self):

@@ -300,6 +300,39 @@ class TileMatchVecEnv:
         self._plans[True].step(self.actions.data_ptr(), int(t), trust, self._stream())
         self._eff_valid = True
 
+    def capture_steps(self, actions=None, ts=None, policy: bool = False, key: int = 12345, first_env: int = 0):
+        """Capture len(ts) batched steps into a HIP graph (tmg_plan_capture):
+        run_graph() then enqueues all of them with one host call, the env
+        groups still overlapping across the steps.  actions: a list of (N,)
+        int32 device tensors, one per step (kept alive by the graph), or
+        policy=True for the in-kernel effective-action policy (step counters
+        ts).  Nothing runs at capture time; the graph assumes the state it is
+        replayed on has this library's own masks (run it right after steps,
+        resets or other graphs of this env)."""
+        ts = list(range(len(actions))) if ts is None else [int(t) for t in ts]
+        self.join()
+        if policy:
+            if self.actions is None:
+                self.actions = torch.zeros(self.num_envs, dtype=torch.int32, device=self.device)
+            if self._policy != (int(key), int(first_env)):
+                self._policy = (int(key), int(first_env))
+                self._configure()
+            ptrs = [self.actions.data_ptr()] * len(ts)
+        else:
+            if len(actions) != len(ts):
+                raise ValueError("one action tensor per step")
+            ptrs = [a.data_ptr() for a in actions]
+        side = torch.cuda.Stream(self.device)          # the NULL stream cannot be captured
+        side.wait_stream(torch.cuda.current_stream(self.device))
+        g = self._plans[bool(policy)].capture(ptrs, ts, int(self._eff_valid), side.cuda_stream)
+        g.refs = (actions, side)
+        return g
+
+    def run_graph(self, graph):
+        """Enqueue a captured run of steps (capture_steps) on the current stream."""
+        graph.launch(self._stream())
+        self._eff_valid = True
+
     def invalidate_effective_cache(self):
         """Call after editing self.board by hand."""
         self._eff_valid = False
