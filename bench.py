@@ -309,13 +309,17 @@ def main():
                                      interleave=args.phase_interleave, shift=shift)
     env.status(clear=True)
 
-    def step(t):
+    rows = [acts[t] for t in range(T)]                    # the staged action rows (views)
+
+    def step(t, fork=True):
+        # fork=False: back-to-back steps on staged actions (nothing queued on
+        # the current stream in between), so the group streams skip the fork
         if venv is not None:
-            venv.step(acts[t % T])                            # obs, rewards, terminations, truncations, infos
+            venv.step(rows[t % T])                            # obs, rewards, terminations, truncations, infos
         elif args.policy == "effective":
-            env.step_effective(t, first_env=rng_.start)       # sampled inside the step kernel
+            env.step_effective(t, first_env=rng_.start, fork=fork)   # sampled inside the step
         else:
-            env.step_raw(acts[t % T])
+            env.step_raw(rows[t % T], fork=fork)
 
     for t in range(args.warmup):
         step(t)
@@ -341,7 +345,7 @@ def main():
     else:
         env.record(ev[2])
         for i in range(args.steps):
-            step(args.warmup + i)
+            step(args.warmup + i, fork=i == 0)
     host_issue_s = time.perf_counter() - t0          # host time to enqueue the window (launch-rate check)
     if graph is None:
         env.record(ev[3])

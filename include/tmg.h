@@ -148,13 +148,15 @@ TMG_API int tmg_plan_config(tmg_plan *plan, int autoreset, int policy, uint64_t 
                             void *onehot, int onehot_dtype, uint8_t *terminated, uint8_t *action_mask,
                             int64_t *moves_left, int8_t *final_board, int32_t *board32);
 
-/* One step of every env: the group streams first wait for the work queued
- * on `stream` (an event), then each group's launches are enqueued on its
+/* One step of every env: with fork != 0 the group streams first wait for
+ * the work queued on `stream` (an event; fork = 0 when nothing queued there
+ * since the previous step is read by this one, e.g. back-to-back steps on
+ * actions staged beforehand), then each group's launches are enqueued on its
  * stream.  Nothing waits for them: call tmg_plan_join before reading the
  * results on `stream`.  actions [n] (input, or the policy's output) must stay
  * valid until then.  t: the step counter of the policy draw.  trust_eff: as
  * tmg_step. */
-TMG_API int tmg_plan_step(tmg_plan *plan, int32_t *actions, int32_t t, int trust_eff, void *stream);
+TMG_API int tmg_plan_step(tmg_plan *plan, int32_t *actions, int32_t t, int trust_eff, int fork, void *stream);
 
 /* `stream` waits for every group's queued work (events). */
 TMG_API int tmg_plan_join(tmg_plan *plan, void *stream);

@@ -555,7 +555,7 @@ int tmg_plan_config(tmg_plan *p, int autoreset, int policy, uint64_t key, int64_
     return 0;
 }
 
-int tmg_plan_step(tmg_plan *p, int32_t *actions, int32_t t, int trust_eff, void *stream) {
+int tmg_plan_step(tmg_plan *p, int32_t *actions, int32_t t, int trust_eff, int fork, void *stream) {
     if (!p) return fail(-1, "null plan");
     if (!actions) return fail(-1, "null actions");
     tmg_ctx *ctx = p->ctx;
@@ -563,9 +563,9 @@ int tmg_plan_step(tmg_plan *p, int32_t *actions, int32_t t, int trust_eff, void 
     if (rc) return rc;
     const hipStream_t cur = reinterpret_cast<hipStream_t>(stream);
     const int G = (int)p->streams.size();
-    bool fork = false;                      // a NULL group stream is the call's own stream
-    for (int g = 0; g < G; g++) fork |= p->streams[g] != nullptr && p->streams[g] != cur;
-    if (fork) {                             // the group streams see the work queued on `stream`
+    bool other = false;                     // a NULL group stream is the call's own stream
+    for (int g = 0; g < G; g++) other |= p->streams[g] != nullptr && p->streams[g] != cur;
+    if (fork && other) {                    // the group streams see the work queued on `stream`
         rc = hip_check(hipEventRecord(p->fork, cur), "hipEventRecord");
         for (int g = 0; g < G && !rc; g++)
             if (p->streams[g] && p->streams[g] != cur)
@@ -655,7 +655,7 @@ int tmg_plan_capture(tmg_plan *p, int steps, int32_t *const *actions, const int3
     gr->device = p->ctx->device;
     rc = hip_check(hipStreamBeginCapture(cur, hipStreamCaptureModeThreadLocal), "hipStreamBeginCapture");
     if (rc) { delete gr; return rc; }
-    for (int k = 0; k < steps && !rc; k++) rc = tmg_plan_step(p, actions[k], t[k], k ? 1 : trust_eff, stream);
+    for (int k = 0; k < steps && !rc; k++) rc = tmg_plan_step(p, actions[k], t[k], k ? 1 : trust_eff, k == 0, stream);
     if (!rc) rc = tmg_plan_join(p, stream);
     const int rc_end = hip_check(hipStreamEndCapture(cur, &gr->graph), "hipStreamEndCapture");
     if (!rc) rc = rc_end;

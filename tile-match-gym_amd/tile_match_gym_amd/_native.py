@@ -87,7 +87,7 @@ def load(path: str = None):
     L.tmg_reset_onehot.argtypes = [P, I64, P, P, P, P, P, P, I, P]
     L.tmg_plan_create.argtypes = [ctypes.POINTER(P), P, I64, P, P, P, P, P, P, P, P, I, P, P]
     L.tmg_plan_config.argtypes = [P, I, I, ctypes.c_uint64, I64, P, I, P, P, P, P, P]
-    L.tmg_plan_step.argtypes = [P, P, ctypes.c_int32, I, P]
+    L.tmg_plan_step.argtypes = [P, P, ctypes.c_int32, I, I, P]
     L.tmg_plan_join.argtypes = [P, P]
     L.tmg_plan_destroy.argtypes = [P]
     L.tmg_plan_capture.argtypes = [P, I, P, P, I, P, ctypes.POINTER(P)]
@@ -262,8 +262,8 @@ class Plan:
                                       int(key) & 0xFFFFFFFFFFFFFFFF, int(first_env), onehot, int(onehot_dtype),
                                       terminated, action_mask, moves_left, final_board, board32), self._L)
 
-    def step(self, actions_ptr: int, t: int, trust_eff: int, stream: int):
-        rc = self._step(self._h, actions_ptr, t, trust_eff, stream)
+    def step(self, actions_ptr: int, t: int, trust_eff: int, stream: int, fork: int = 1):
+        rc = self._step(self._h, actions_ptr, t, trust_eff, fork, stream)
         if rc:
             check(rc, self._L)
 

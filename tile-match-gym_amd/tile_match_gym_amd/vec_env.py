@@ -267,19 +267,22 @@ class TileMatchVecEnv:
         done = (flags & _native.FLAG_DONE) != 0
         return self._obs(), self.reward, done, torch.zeros_like(done), info
 
-    def step_raw(self, actions_i32: torch.Tensor):
+    def step_raw(self, actions_i32: torch.Tensor, fork: bool = True):
         """Enqueue one batched step (no output post-processing): the bench path.
         actions_i32: contiguous int32 (N,) on the device.  With groups > 1 call
         join() before reading results.  One host call (tmg_plan_step) enqueues
-        every group's launches; the actions tensor is held until join()."""
-        self._plans[False].step(actions_i32.data_ptr(), 0, int(self._eff_valid), self._stream())
+        every group's launches; the actions tensor is held until join().
+        fork=False: nothing queued on the current stream since the previous
+        step is read by this one (e.g. actions staged beforehand), so the group
+        streams need not wait for it (saves the fork event per step)."""
+        self._plans[False].step(actions_i32.data_ptr(), 0, int(self._eff_valid), self._stream(), int(fork))
         self._eff_valid = True
         if self._streams:
             self._held.append(actions_i32)
             if len(self._held) > 256:
                 self.join()
 
-    def step_effective(self, t: int, key: int = 12345, first_env: int = 0):
+    def step_effective(self, t: int, key: int = 12345, first_env: int = 0, fork: bool = True):
         """Enqueue one step of the examples' policy (src/examples/q_learning.py:19-25):
         every env takes an action drawn uniformly from its effective actions
         (tmg_sample_effective's draw, counter-based in (key, first_env + env, t),
@@ -297,7 +300,7 @@ class TileMatchVecEnv:
             self.join()
             self._policy = (int(key), int(first_env))
             self._configure()
-        self._plans[True].step(self.actions.data_ptr(), int(t), trust, self._stream())
+        self._plans[True].step(self.actions.data_ptr(), int(t), trust, self._stream(), int(fork))
         self._eff_valid = True
 
     def capture_steps(self, actions=None, ts=None, policy: bool = False, key: int = 12345, first_env: int = 0):
