@@ -78,17 +78,20 @@ abx)
   done
   ;;
 pmcmb)
+  # SQ counts per launch kind; TREE=base: the _ab_base/ worktree (previous commit) with its own library
+  dir=$PWD; tag=""
+  [ "${TREE:-}" = base ] && { dir=$PWD/_ab_base; tag=_base; }
   for c in ${CONFIGS:-c2 c5}; do
     i=0
     for set in "SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_SMEM SQ_WAVES SQ_INSTS_BRANCH SQ_WAVE_CYCLES SQ_BUSY_CYCLES" \
                "SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_SCA SQ_WAIT_ANY SQ_ACTIVE_INST_ANY"; do
       i=$((i+1))
-      timeout -s KILL 150 rocprofv3 --pmc $set --kernel-trace -d $OUT/pmcmb_${c}_$i -o run --output-format csv -- \
-        python3 tools/microbench.py --config $c > $OUT/pmcmb_${c}_$i.log 2>&1 || { echo "pmc $c $i failed"; tail -5 $OUT/pmcmb_${c}_$i.log; exit 1; }
+      (cd $dir && timeout -s KILL 150 rocprofv3 --pmc $set --kernel-trace -d $OUT/pmcmb${tag}_${c}_$i -o run --output-format csv -- \
+        python3 tools/microbench.py --config $c) > $OUT/pmcmb${tag}_${c}_$i.log 2>&1 || { echo "pmc $c $i failed"; tail -5 $OUT/pmcmb${tag}_${c}_$i.log; exit 1; }
     done
     nb=$(python3 -c "import bench; print(bench.CONFIGS['$c'][5])")
-    python3 tools/pmc_micro.py $OUT/pmcmb_${c}_1 $OUT/pmcmb_${c}_2 --boards $nb --eff-frac 0.24 > $OUT/pmcmb_${c}.json \
-      && echo "$c" && head -c 600 $OUT/pmcmb_${c}.json
+    python3 tools/pmc_micro.py $OUT/pmcmb${tag}_${c}_1 $OUT/pmcmb${tag}_${c}_2 --boards $nb --eff-frac 0.24 > $OUT/pmcmb${tag}_${c}.json \
+      && echo "$c$tag" && head -c 300 $OUT/pmcmb${tag}_${c}.json
   done
   ;;
 window)

@@ -6,6 +6,8 @@ quick   : every env takes the ineffective-move exit (cached mask all zero,
           timer kept below num_moves) -> the dispatch + per-env I/O floor.
 normal  : the bench's action stream, steps 1..28 of an episode (no autoreset).
 storm   : the autoreset step (every env regenerates its board).
+policy  : a step of the effective-action policy (bench --policy effective):
+          every env plays an effective move.
 Times are HIP-event device times per launch (median of the probes).
 """
 import argparse
@@ -68,6 +70,13 @@ def main():
         q += timed(quick, 1)
     res["quick_us"] = statistics.median(q)
     env.eff.copy_(saved_eff)
+    # the examples' policy: every env plays one of its effective actions
+    # (bench --policy effective), timers held below the episode end
+    pol = []
+    for t in range(20):
+        env.timer.zero_()
+        pol += timed(lambda: env.step_effective(t), 1)
+    res["policy_us"] = statistics.median(pol)
     print({k: round(v, 2) for k, v in res.items()}, flush=True)
 
 

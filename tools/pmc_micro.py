@@ -6,7 +6,9 @@
 
 microbench.py launches, in order: 60 steps of the bench's action stream (the
 autoreset storm at steps 29 and 59, normal steps otherwise), then 20
-quick-exit launches (every move ineffective).  Each step is one step_kernel
+quick-exit launches (every move ineffective), then 20 steps of the
+effective-action policy ("policy": every env plays an effective move; the
+general kernels' sampler kernel ahead of each is not counted).  Each step is one step_kernel
 launch, plus, for the general / 512-cell kernels, a spill_kernel launch and a
 reset_kernel launch masked by FL_RESET (the deferred autoreset).  This prints
 the median count per env of each counter over the normal, storm and quick
@@ -47,8 +49,10 @@ def main():
         for i, k in enumerate(steps):
             if i < 60:
                 cats["storm" if i % 30 == 29 else "normal"].append(per[k])
-            else:
+            elif i < 80:
                 cats["quick"].append(per[k])
+            else:
+                cats["policy"].append(per[k])
         # the masked reset / spill launches that follow step i (before step i + 1)
         first = steps[0][1] if steps else None
         si = -1
