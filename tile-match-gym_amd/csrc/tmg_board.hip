@@ -2304,8 +2304,9 @@ __device__ __forceinline__ uint32_t step_env(
     constexpr bool INLINE_GEN = !GEN && MAXN == 128;
     const bool same = autoreset == 1 || autoreset == 2;
     const bool regen_inline = autoreset == 1 || autoreset == 3;
-    int a = 0;
-    if (!P.sample) a = __builtin_amdgcn_readfirstlane(actions[e]);       // wave-uniform loads
+    // wave-uniform loads (the action too with the in-kernel policy, where the
+    // draw below replaces it: no wait for the flag before the load goes out)
+    int a = __builtin_amdgcn_readfirstlane(actions[e]);
     const int t0 = __builtin_amdgcn_readfirstlane(timer[e]);
     // Issued beside the two loads above, not depending on the action: the
     // env's cached mask row (lane i holds word i).  The ineffective-move exit
@@ -2315,25 +2316,6 @@ __device__ __forceinline__ uint32_t step_env(
     // state there too measured slower: the quick waves wait for those loads.
     const uint64_t effrow = lane < W ? eff[e * W + lane] : 0ULL;
     TMG_KEEP_V(effrow);
-    // The effective path's loads issued together, before anything waits on
-    // one: the board (when whole dwords), the RNG state and this lane's
-    // jump-table row.  One memory round trip instead of three dependent ones
-    // (board -> LDS -> precondition -> RNG -> jump table).  With the in-kernel
-    // policy every move is effective, so they go out with the mask row;
-    // otherwise after the ineffective-move exit.
-    int8_t *gb = board + e * 2 * N;
-    const int nbw = (2 * N) >> 2;
-    const bool bwhole = ((2 * N) & 3) == 0 && nbw <= 64;
-    uint32_t bw = 0;
-    uint64_t q0 = 0, q1 = 0, q2 = 0, q3 = 0, q4 = 0, j0 = 0, j1 = 0, j2 = 0, j3 = 0;
-    const auto issue_loads = [&]() {
-        bw = bwhole ? reinterpret_cast<const uint32_t *>(gb)[lane < nbw ? lane : 0] : 0u;
-        const uint64_t *rp = rng + e * 5;
-        q0 = rp[0]; q1 = rp[1]; q2 = rp[2]; q3 = rp[3]; q4 = rp[4];
-        const uint64_t *jt = P.jump + lane * 4;
-        j0 = jt[0]; j1 = jt[1]; j2 = jt[2]; j3 = jt[3];
-    };
-    if (P.sample) issue_loads();
     if (P.sample) {                                                         // the policy's action, from the mask
         a = __builtin_amdgcn_readfirstlane(sample_action(P, effrow, e));
         if (lane == 0) const_cast<int32_t *>(actions)[e] = a;
@@ -2352,6 +2334,7 @@ __device__ __forceinline__ uint32_t step_env(
         }
         return ST_CALLER;
     }
+    int8_t *gb = board + e * 2 * N;
     uint64_t *ge = eff + e * W;
     const int t1 = t0 + 1;
     const bool done = !pend && t1 == P.num_moves;                           // tile_match_env.py:100-101
@@ -2369,6 +2352,7 @@ __device__ __forceinline__ uint32_t step_env(
             if (P.vo_mask) store_mask(P, w, lane, e, true);
         }
         if (done && same && P.vo_final) {                                   // the last board, as it stands
+            const int nbw = (2 * N) >> 2;
             const uint32_t *src = reinterpret_cast<const uint32_t *>(gb);
             uint32_t *dst = reinterpret_cast<uint32_t *>(P.vo_final + e * 2 * N);
             for (int i = lane; i < nbw; i += 64) dst[i] = src[i];
@@ -2386,7 +2370,19 @@ __device__ __forceinline__ uint32_t step_env(
     action_coords(P.R, P.C, a, r1, c1, r2, c2);
     const int p1 = r1 * P.C + c1, p2 = r2 * P.C + c2;
 
-    if (!P.sample) issue_loads();
+    // The effective path's loads issued together, before anything waits on
+    // one: the board (when whole dwords), the RNG state and this lane's
+    // jump-table row.  One memory round trip instead of three dependent ones
+    // (board -> LDS -> precondition -> RNG -> jump table).  (Issued with the
+    // mask row instead when the in-kernel policy makes every move effective:
+    // measured the same, c2 4.76 vs 4.75 x 10^8, and it cost the quick exit.)
+    const int nbw = (2 * N) >> 2;
+    const bool bwhole = ((2 * N) & 3) == 0 && nbw <= 64;
+    const uint32_t bw = bwhole ? reinterpret_cast<const uint32_t *>(gb)[lane < nbw ? lane : 0] : 0u;
+    const uint64_t *rp = rng + e * 5;
+    const uint64_t q0 = rp[0], q1 = rp[1], q2 = rp[2], q3 = rp[3], q4 = rp[4];
+    const uint64_t *jt = P.jump + lane * 4;
+    const uint64_t j0 = jt[0], j1 = jt[1], j2 = jt[2], j3 = jt[3];
     if (bwhole) {
         if (lane < nbw) reinterpret_cast<uint32_t *>(w.brd)[lane] = bw;
     } else {
