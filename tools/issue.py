@@ -9,10 +9,10 @@ Each `<run>` directory holds one `--pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_WAVES
 effective-action policy), and `<run>.log` that run's bench line, whose build
 hash, policy, boards and env groups are recorded with the counts (bench.py
 attaches a profile only to a line of the same build and run shape).
-Counted: every step_kernel dispatch and every reset_kernel dispatch issued
-after the first step_kernel one (the deferred autoreset launches of the
-512-cell / general kernels are part of a step); the initial reset() launch is
-not.  Env-steps = (S + W) x boards of the config (bench.CONFIGS).
+Counted: every step_kernel dispatch and every reset_kernel / sampler dispatch
+issued after the first step_kernel one (the deferred autoreset launches of the
+512-cell / general kernels and the policy draw ahead of the general kernels
+are part of a step); the initial reset() launch is not.  Env-steps = (S + W) x boards of the config (bench.CONFIGS).
 """
 import collections
 import csv
@@ -61,7 +61,7 @@ def main():
             nm = names[i]
             if "step_kernel" in nm:
                 n_step += 1
-            elif "reset_kernel" in nm and i > first_step:
+            elif ("reset_kernel" in nm or "sample_effective_kernel" in nm) and i > first_step:
                 n_reset += 1
             else:
                 continue
@@ -79,7 +79,7 @@ def main():
             # the bench run these counts belong to (bench.py attaches them only to a line of the same build and
             # run shape)
             **bench.run_identity(line),
-            "dispatches": {"step_kernel": n_step, "reset_kernel": n_reset},
+            "dispatches": {"step_kernel": n_step, "reset_or_sampler_kernel": n_reset},
             "source": (f"rocprofv3 --pmc {' '.join(COUNTERS)} --kernel-trace, bench.py {' '.join(bench.run_args(name))} "
                        f"(steps + warmup = {steps}); scripts/gpu_issue.sh, tools/issue.py"),
         }

@@ -17,8 +17,9 @@ import sys
 
 
 def per_dispatch(path, counter, with_resets=False):
-    """KiB per step_kernel dispatch; with_resets: also the reset_kernel
-    dispatches after the first step_kernel one (deferred autoresets)."""
+    """KiB per step_kernel dispatch; with_resets: also the reset_kernel and
+    sampler dispatches after the first step_kernel one (deferred autoresets,
+    the policy draw ahead of the general kernels)."""
     vals = collections.defaultdict(float)
     names = {}
     for f in glob.glob(os.path.join(path, "**", "*counter_collection.csv"), recursive=True):
@@ -31,7 +32,8 @@ def per_dispatch(path, counter, with_resets=False):
     steps = sorted(d for d in vals if "step_kernel" in names[d])
     keep = set(steps)
     if with_resets and steps:
-        keep |= {d for d in vals if "reset_kernel" in names[d] and d > steps[0]}
+        keep |= {d for d in vals if ("reset_kernel" in names[d] or "sample_effective_kernel" in names[d])
+                 and d > steps[0]}
     return [vals[d] for d in sorted(keep)]
 
 
