@@ -2320,8 +2320,14 @@ __device__ __forceinline__ uint32_t step_env(
         a = __builtin_amdgcn_readfirstlane(sample_action(P, effrow, e));
         if (lane == 0) const_cast<int32_t *>(actions)[e] = a;
     }
-    const bool pend = autoreset >= 3 && t0 >= P.num_moves;                 // ended last call: reset() now
-    if (!pend && (t0 >= P.num_moves || a < 0 || a >= P.A)) {                // tile_match_env.py:94-95
+    // an env that ended last call, with next-step autoreset: reset() now
+    // (tested only inside the rare branch, so that the common path carries
+    // no extra condition into the ineffective-move exit)
+    bool pend = false;
+    if (t0 >= P.num_moves || a < 0 || a >= P.A) {                           // tile_match_env.py:94-95
+        pend = autoreset >= 3 && t0 >= P.num_moves;
+    }
+    if (!pend && (t0 >= P.num_moves || a < 0 || a >= P.A)) {
         if (lane == 0) {
             reward[e] = 0; n_new[e] = 0; n_act[e] = 0; flags_out[e] = FL_ERR;
             store_vo(P, e, FL_ERR, t0);
