@@ -415,6 +415,18 @@ struct LaneJump {
     U128 Aj, Gj, incG;    // A^{lane+1}, G_{lane+1}, G_{lane+1} * inc
 };
 
+// jump128's f operand goes through SGPRs (pcg64.h): it must be wave-uniform,
+// or the compiler silently takes lane 0's value.  TMG_COVER builds check every
+// call site's f and raise ST_INTERNAL on a divergent one.
+__device__ __forceinline__ void cover_uniform(const Params &P, int lane, U128 f) {
+#if TMG_COVER
+    const bool div = f.lo != bcast64(f.lo) || f.hi != bcast64(f.hi);
+    if (__ballot(div) != 0 && lane == 0) P.status[0] = 1u;
+#else
+    (void)P; (void)lane; (void)f;
+#endif
+}
+
 // single-lane stream (serial replays, shuffle)
 __device__ __forceinline__ uint64_t r_next64(Rng &g) {
     U128 s = add128(mul128(U128{g.slo, g.shi}, U128{PCG_A_LO, PCG_A_HI}), U128{g.ilo, g.ihi});
@@ -473,6 +485,7 @@ __device__ __forceinline__ void draw_colours(const Params &P, int lane, const La
     U128 sj{0, 0};
     uint64_t out = 0;
     for (int base = 0; base < n64; base += 64) {
+        cover_uniform(P, lane, s);
         sj = jump128(J.Aj, s, J.incG);
         out = xsl_rr(sj);
         const int j = base + lane;
@@ -1194,6 +1207,7 @@ __device__ __forceinline__ void bp_ring_init(const Params &P, WS &w, int lane, c
     // table row and its product with inc would otherwise be hoisted out of
     // the loop and held in 8 VGPRs through every redraw)
     const uint64_t *t = P.jump + bp_out(loop_lane(lane)) * 4;
+    cover_uniform(P, lane, U128{g.slo, g.shi});
     J.X = jump128(U128{t[0], t[1]}, U128{g.slo, g.shi}, mul128(U128{g.ilo, g.ihi}, U128{t[2], t[3]}));
 }
 
@@ -1205,6 +1219,7 @@ template <int NB, class WS>
 __device__ __forceinline__ void bp_ring_fill(const Params &P, WS &w, int lane, BpJump &J, BpRing &r) {
     const uint32_t k = (uint32_t)P.k;
     const uint64_t out = xsl_rr(J.X);
+    cover_uniform(P, lane, J.A64);
     J.X = jump128(J.X, J.A64, J.c64);                                // the next batch (A^64: uniform, SGPRs)
     const uint64_t m0 = (uint64_t)(uint32_t)out * k, m1 = (out >> 32) * k;
     if (P.thr != 0u) r.rmin = umin3(r.rmin, (uint32_t)m0, (uint32_t)m1);   // tested once, after the redraws

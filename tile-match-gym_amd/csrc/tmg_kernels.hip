@@ -103,9 +103,7 @@ void launch_step512(bool gen, dim3 grid, hipStream_t s, const Params &P, const S
 void launch_reset512(dim3 grid, hipStream_t s, const Params &P, int64_t n, int8_t *board, uint64_t *rng,
                      int32_t *timer, uint64_t *eff, const uint8_t *env_mask, int mask_bits, int epw) {
     // NB = colour bit-planes of the row-plane generate (bp_generate)
-#ifndef TMG_NOFIX_RESET20
     if (is_shape<kFixReset20>(P)) { reset_one<512, 3, false, kFixReset20>(grid, s, P, n, board, rng, timer, eff, env_mask, mask_bits, epw); return; }
-#endif
     switch (sb_planes(P.k)) {
     case 1: reset_one<512, 1, false>(grid, s, P, n, board, rng, timer, eff, env_mask, mask_bits, epw); break;
     case 2: reset_one<512, 2, false>(grid, s, P, n, board, rng, timer, eff, env_mask, mask_bits, epw); break;

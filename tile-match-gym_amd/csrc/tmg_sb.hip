@@ -395,6 +395,7 @@ __device__ __forceinline__ int sb_ensure(const Params &P, WS &w, int lane, const
     for (int shuffles = 0;; shuffles++) {
         if (!clean) {
             for (;;) {
+                cover_uniform(P, lane, U128{g.slo, g.shi});
                 const SBDrawPre pre = sb_draw_pre(J, g);
                 const SBDet d = sb_detect<NB, CODD>(P, sb_planes_of<NB>(c));
                 const int key = sb_first_line_key<NB, CODD>(P, d, lane, keyA, keyB);
@@ -433,6 +434,7 @@ template <int NB, bool CODD, class WS>
 __device__ __forceinline__ int sb_generate_exact(const Params &P, WS &w, int lane, const LaneJump &J, Rng &g,
                                                  const Cells<WS::NP> &cl) {
     SBC c{0, 0};
+    cover_uniform(P, lane, U128{g.slo, g.shi});
     sb_draw_rows<NB>(P, w, lane, J, g, P.R - 1, c, sb_draw_pre(J, g));
     for (int p = lane; p < P.N; p += 64) w.brd[P.N + p] = 1;
     return sb_ensure<NB, CODD, true>(P, w, lane, J, g, cl, c, true, false) & FL_ERR;
