@@ -59,6 +59,9 @@ CONFIGS = {
     "c2": (10, 10, 4, [], [], 65536, "no specials"),
     "c3": (10, 10, 4, [], ["vertical_laser", "horizontal_laser", "bomb"], 262144, "v/h-laser + bomb"),
     "c5": (20, 20, 6, ["cookie"], ["vertical_laser", "horizontal_laser", "bomb"], 262144, "all specials"),
+    # shapes no kernel is specialised for (tmg_kernels.hip is_shape): the generic instantiations' rate
+    "g1": (10, 10, 5, [], [], 65536, "no specials, generic kernels"),
+    "g2": (20, 20, 6, [], ["vertical_laser", "horizontal_laser", "bomb"], 262144, "v/h-laser + bomb, generic kernels"),
 }
 
 
