@@ -653,32 +653,27 @@ __host__ __device__ __forceinline__ uint64_t policy_draw(uint64_t key, uint64_t 
 // tmg_sample_effective's draw for env e inside the step (Params::sample):
 // the r-th set bit of the env's mask, r = h * count >> 32, or h * A >> 32 when
 // no action is effective.  effrow: lane i holds mask word i (W <= 64).
-// Wave-uniform, on the scalar unit: the words by readlane, the r-th set bit of
-// the chosen word by a binary search on popcounts.
-__device__ __forceinline__ int sample_action(const Params &P, uint64_t effrow, int64_t e) {
-    const uint64_t h = policy_draw(P.pol_key, (uint64_t)(P.pol_first + e), P.pol_t);
+// The word holding bit r by readlanes of the per-lane popcounts; inside it,
+// the lane whose bit is set with r set bits below it (v_mbcnt) is the action:
+// a handful of VALU and one ballot instead of a scalar binary search (the
+// scalar unit is the step kernels' busiest pipe).
+__device__ __forceinline__ int sample_action(const Params &P, uint64_t effrow, int64_t e, int lane) {
+    const uint32_t h = (uint32_t)policy_draw(P.pol_key, (uint64_t)(P.pol_first + e), P.pol_t);
     const int W = P.W;
+    const int pc = __popcll(effrow);                    // 0 on lanes >= W
     int count = 0;
-    for (int j = 0; j < W; j++) count += __popcll(rdlane64(effrow, j));
-    if (count == 0) return (int)((h * (uint64_t)P.A) >> 32);
-    int r = (int)((h * (uint64_t)count) >> 32);
-    int a = 0;
-    for (int j = 0; j < W; j++) {
-        uint64_t x = rdlane64(effrow, j);
-        const int c = __popcll(x);
-        if (r < c) {
-            int pos = 0;
-#pragma unroll
-            for (int s = 32; s >= 1; s >>= 1) {
-                const int cl = __popcll(x & ((1ULL << s) - 1ULL));
-                if (r >= cl) { r -= cl; x >>= s; pos += s; }
-            }
-            a = j * 64 + pos;
-            break;
-        }
+    for (int j = 0; j < W; j++) count += __builtin_amdgcn_readlane(pc, j);
+    if (count == 0) return (int)(((uint64_t)h * (uint64_t)P.A) >> 32);
+    int r = (int)(((uint64_t)h * (uint64_t)count) >> 32);
+    int j = 0;
+    for (; j < W - 1; j++) {
+        const int c = __builtin_amdgcn_readlane(pc, j);
+        if (r < c) break;
         r -= c;
     }
-    return a;
+    const uint64_t x = rdlane64(effrow, j);
+    const bool hit = ((x >> lane) & 1ULL) && popc_below(x) == r;
+    return j * 64 + __ffsll((unsigned long long)__ballot(hit)) - 1;
 }
 
 // is_move_effective, board.py:735-787 — exact windowed scan (any board)
@@ -2332,7 +2327,7 @@ __device__ __forceinline__ uint32_t step_env(
     const uint64_t effrow = lane < W ? eff[e * W + lane] : 0ULL;
     TMG_KEEP_V(effrow);
     if (P.sample) {                                                         // the policy's action, from the mask
-        a = __builtin_amdgcn_readfirstlane(sample_action(P, effrow, e));
+        a = __builtin_amdgcn_readfirstlane(sample_action(P, effrow, e, lane));
         if (lane == 0) const_cast<int32_t *>(actions)[e] = a;
     }
     // an env that ended last call, with next-step autoreset: reset() now
