@@ -44,12 +44,6 @@ constexpr int kC5StepWaves = 4;      // step_kernel<512, true> specialised for c
 
 // compiler-only ordering point between a wave's LDS loads and later stores
 #define WFENCE() __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront")
-// an empty asm reading eight VGPR values: all of them are loaded (and their
-// loads issued) before anything after it
-#ifndef TMG_KEEP_V8
-#define TMG_KEEP_V8(a, b, c, d, e, f, g, h) \
-    asm volatile("" ::"v"(a), "v"(b), "v"(c), "v"(d), "v"(e), "v"(f), "v"(g), "v"(h))
-#endif
 
 // dynamic LDS of the workgroup (overridable only by the host-side wave
 // emulator in tools/wave_emu, which runs this file under AddressSanitizer)
@@ -1280,8 +1274,8 @@ __device__ __forceinline__ bool bp_rejected(const Params &P, const BpRing &r) {
 
 // The exact PCG64 state after the last consumed colour i: lane L = the lane
 // of its output o holds X = s_{n+1} for output n = o of the next unfilled
-// batch, m = (fill >> 7) - (i >> 7) batches after i's (1 <= m <= 3: a take
-// leaves fewer than 256 colours filled ahead), so s = A^{-64m} X - A^{-64m}
+// batch, m = (fill >> 7) - (i >> 7) batches after i's (1 <= m <= 6: the
+// redraw loop keeps fewer than N + 128 <= 640 colours filled ahead), so s = A^{-64m} X - A^{-64m}
 // G_{64m} inc (jump-table row 63 + m).
 __device__ __forceinline__ void bp_ring_state(const Params &P, const BpJump &J, const BpRing &r, Rng &g) {
     if (r.cons == r.cons0) return;                                   // nothing taken since bp_ring_init(g)
@@ -1297,42 +1291,55 @@ __device__ __forceinline__ void bp_ring_state(const Params &P, const BpJump &J, 
     g.h = ((uint64_t)((local & 1) ^ 1) << 32) | (uint32_t)(xsl_rr(U128{g.slo, g.shi}) >> 32);   // lo half taken: hi half buffered
 }
 
-// rows 0..row <- the ring's next (row + 1) * C colours (colour plane only)
-// AHEAD: the next redraw's batch is filled (when fewer than 128 colours would
-// be left) between issuing the ring reads and using them, under their latency
-template <int NB, bool AHEAD = false, class WS>
-__device__ __forceinline__ void bp_take(const Params &P, WS &w, int lane, BpJump &J, BpRing &r, int row,
-                                        uint32_t cm, RowPlanes<NB> &pl) {
-    const int M = (row + 1) * P.C;
-    r.fill = __builtin_amdgcn_readfirstlane(r.fill);             // wave-uniform (see bp_generate)
+// The next redraw's colours start at the ring's consume position whatever rows
+// it redraws (lane r's row at cons + rC), so its reads can be issued before the
+// line search that decides the rows: bp_prefetch keeps at least maxM colours
+// filled ahead and issues every plane's two ring dwords, bp_apply merges rows
+// 0..row once the search has returned.  The LDS latency then overlaps the
+// search instead of following it.
+template <int NB>
+struct BpReads {
+    uint32_t lo[NB], hi[NB], sh;
+};
+template <int NB, class WS>
+__device__ __forceinline__ BpReads<NB> bp_prefetch(const Params &P, WS &w, int lane, BpJump &J, BpRing &r, int maxM) {
+    r.fill = __builtin_amdgcn_readfirstlane(r.fill);
     r.cons = __builtin_amdgcn_readfirstlane(r.cons);
-    while (r.fill - r.cons < M) bp_ring_fill<NB>(P, w, lane, J, r);
+    while (r.fill - r.cons < maxM) bp_ring_fill<NB>(P, w, lane, J, r);
     // One wave per workgroup, and a wave's LDS instructions execute in order:
     // the reads below see lane 0's ring stores (bp_ring_fill) without waiting
     // for those stores to complete, so a compiler-only fence, not WSYNC's wait
     WFENCE();
     const uint32_t *ring = bp_ring(w);
-    const int o = r.cons + lane * P.C;                           // this lane's row starts here
+    const int o = r.cons + lane * P.C;
     const int d = (o >> 5) & (kBpRingDw - 1);
-    const uint32_t s = (uint32_t)o & 31u;
-    const uint32_t in = lane <= row ? cm : 0u;                   // the cells this take rewrites
-    uint32_t lo[NB], hi[NB];                                     // every plane's reads issued together:
-#pragma unroll                                                   // one LDS round trip per take (the
-    for (int b = 0; b < NB; b++) {                               // scheduler otherwise waits for plane 0
-        lo[b] = ring[b * kBpPlaneDw + d];                        // before issuing the others)
-        hi[b] = ring[b * kBpPlaneDw + d + 1];
-    }
-    if constexpr (AHEAD) {
-        if (r.fill - r.cons - M < 128) bp_ring_fill<NB>(P, w, lane, J, r);
-    }
-    TMG_KEEP_V8(lo[0], hi[0], lo[NB > 1 ? 1 : 0], hi[NB > 1 ? 1 : 0], lo[NB > 2 ? 2 : 0], hi[NB > 2 ? 2 : 0],
-                lo[NB > 3 ? 3 : 0], hi[NB > 3 ? 3 : 0]);
+    BpReads<NB> x;
+    x.sh = (uint32_t)o & 31u;
 #pragma unroll
     for (int b = 0; b < NB; b++) {
-        const uint32_t v = __builtin_amdgcn_alignbit(hi[b], lo[b], s);
+        x.lo[b] = ring[b * kBpPlaneDw + d];
+        x.hi[b] = ring[b * kBpPlaneDw + d + 1];
+    }
+    return x;
+}
+template <int NB>
+__device__ __forceinline__ void bp_apply(const Params &P, int lane, BpRing &r, const BpReads<NB> &x, int row, uint32_t cm,
+                                         RowPlanes<NB> &pl) {
+    const uint32_t in = lane <= row ? cm : 0u;
+#pragma unroll
+    for (int b = 0; b < NB; b++) {
+        const uint32_t v = __builtin_amdgcn_alignbit(x.hi[b], x.lo[b], x.sh);
         pl.p[b] = (v & in) | (pl.p[b] & ~in);
     }
-    r.cons += M;
+    r.cons += (row + 1) * P.C;
+}
+
+// rows 0..row <- the ring's next (row + 1) * C colours (colour plane only)
+template <int NB, class WS>
+__device__ __forceinline__ void bp_take(const Params &P, WS &w, int lane, BpJump &J, BpRing &r, int row,
+                                        uint32_t cm, RowPlanes<NB> &pl) {
+    const BpReads<NB> x = bp_prefetch<NB>(P, w, lane, J, r, (row + 1) * P.C);
+    bp_apply<NB>(P, lane, r, x, row, cm, pl);
 }
 
 // The row of the first coord of the first line get_colour_lines would return
@@ -1427,9 +1434,10 @@ __device__ __forceinline__ int bp_generate(const Params &P, WS &w, int lane, Rng
         // rejected word are still colours, the loop ends as it would on any
         // other board, and the board is then redone exactly.
         for (;;) {
+            const BpReads<NB> x = bp_prefetch<NB>(P, w, lane, J, r, N);          // the next redraw's colours
             const int r0 = bp_first_line_row<NB>(pl, hml, vml);
             if (r0 < 0) break;
-            bp_take<NB, true>(P, w, lane, J, r, R - 1 < r0 + 1 ? R - 1 : r0 + 1, cm, pl);   // rows 0..min(R-1, r0+1)
+            bp_apply<NB>(P, lane, r, x, R - 1 < r0 + 1 ? R - 1 : r0 + 1, cm, pl);   // rows 0..min(R-1, r0+1)
         }
         if ((rej = bp_rejected(P, r))) break;
         bp_to_lds<NB>(P, w, lane, pl);

@@ -79,7 +79,6 @@ inline unsigned emu_mbcnt_hi(unsigned m, unsigned acc) {
 #define __builtin_amdgcn_mbcnt_lo(m, a) emu_mbcnt_lo((m), (a))
 #define __builtin_amdgcn_mbcnt_hi(m, a) emu_mbcnt_hi((m), (a))
 #define TMG_OPAQUE_V(x) ((void)0)
-#define TMG_KEEP_V8(a, b, c, d, e, f, g, h) ((void)0)
 
 #define TMG_CONST_AS
 #define TMG_KEEP_V3(x, y, z) ((void)0)
