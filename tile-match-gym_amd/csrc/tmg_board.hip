@@ -1410,6 +1410,10 @@ __device__ __forceinline__ RowPlanes<NB> bp_from_lds(const Params &P, const WS &
 template <int NB, class WS>
 __device__ __forceinline__ int bp_generate(const Params &P, WS &w, int lane, Rng &g) {
     const int R = P.R, C = P.C, N = P.N;
+    // A launch that regenerates boards lasts as long as its slowest board, one
+    // serial chain of redraws on one wave, while the other streams' steps
+    // share its SIMD: the regenerating wave goes first at issue
+    __builtin_amdgcn_s_setprio(3);
     // g is wave-uniform; said so explicitly, since where the divergence analysis
     // cannot see it (the lean step kernel's inline autoreset) the ring's
     // counters and state otherwise go to VGPRs and its loops run exec-masked
@@ -1452,6 +1456,7 @@ __device__ __forceinline__ int bp_generate(const Params &P, WS &w, int lane, Rng
         fl = FL_SHUF;
         bp_ring_init<NB>(P, w, lane, g, r, J);
     }
+    __builtin_amdgcn_s_setprio(0);
     if (rej) {
         COVER(CV_REJECT_GEN);
         g = g0;

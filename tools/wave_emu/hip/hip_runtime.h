@@ -78,6 +78,7 @@ inline unsigned emu_mbcnt_hi(unsigned m, unsigned acc) {
 }
 #define __builtin_amdgcn_mbcnt_lo(m, a) emu_mbcnt_lo((m), (a))
 #define __builtin_amdgcn_mbcnt_hi(m, a) emu_mbcnt_hi((m), (a))
+#define __builtin_amdgcn_s_setprio(p) ((void)0)
 #define TMG_OPAQUE_V(x) ((void)0)
 
 #define TMG_CONST_AS
