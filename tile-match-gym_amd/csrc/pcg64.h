@@ -60,17 +60,13 @@ __host__ __device__ __forceinline__ U128 add128(U128 a, U128 b) {
 // G_64 inc of the row-plane generate's lane-local batches).  f MUST be
 // wave-uniform: its limbs are "s" operands, and for a value the compiler
 // holds in VGPRs it inserts a v_readfirstlane, i.e. every lane would get lane
-// 0's f.  Device: ten
-// v_mad_u64_u32, whose 64-bit addends carry the next limb's partial sum and
-// whose carry-outs (SGPR masks) are added back with v_addc: the 32-bit limbs
-// r0..r3 of the result are
-//   P = a0 f0 + (g1:g0)            r0 = P.lo                 carry c1 -> r2
-//   Q = a0 f1 + (g2:P.hi)          (at 2^32)                 carry c2 -> r3
-//   R = a1 f0 + Q                  r1 = R.lo                 carry c3 -> r3
-//   S = a0 f2 + (g3:R.hi); T = a1 f1 + S; U = a2 f0 + T   (at 2^64, carries >= 2^128)
-//   r2 = U.lo + c1 (carry c4);  r3 = lo32(U.hi + a0 f3 + a1 f2 + a2 f1 + a3 f0) + c2 + c3 + c4
-// (the compiler's lowering of mul128 + add128 issues 16 multiplies and a
-// dozen moves for the same value).
+// 0's f.  Device: ten v_mad_u64_u32 / v_mul_lo_u32 in three short chains
+// (below), whose carry-outs (SGPR masks) are added back with v_addc.  Round 4
+// chained all ten through their 64-bit addends (P = a0 f0 + g.lo, Q = a0 f1 +
+// (g2:P.hi), R = a1 f0 + Q, S = a0 f2 + (g3:R.hi), ... ten deep); the same
+// multiplies three deep measured c2 +2 %, its 20-step window +3.5 %, c5 +2 %
+// (profiles/r05/s15).  The compiler's lowering of mul128 + add128 issues 16
+// multiplies and a dozen moves for the same value.
 #if defined(__HIP_DEVICE_COMPILE__)
 __device__ __forceinline__ uint64_t mad64c(uint32_t a, uint32_t b, uint64_t c, uint64_t &carry) {   // a*b + c, carry out
     uint64_t d;
@@ -82,25 +78,33 @@ __device__ __forceinline__ uint32_t addc32(uint32_t x, uint64_t cin, uint64_t &c
     asm("v_addc_co_u32_e64 %0, %1, %2, 0, %3" : "=v"(r), "=s"(cout) : "v"(x), "s"(cin));
     return r;
 }
+__device__ __forceinline__ uint32_t addc32v(uint32_t x, uint32_t y, uint64_t cin, uint64_t &cout) {   // x + y + carry-in bit
+    uint32_t r;
+    asm("v_addc_co_u32_e64 %0, %1, %2, %3, %4" : "=v"(r), "=s"(cout) : "v"(x), "v"(y), "s"(cin));
+    return r;
+}
 #endif
 __host__ __device__ __forceinline__ U128 add128(U128 a, U128 b);
 __host__ __device__ __forceinline__ U128 jump128(const U128 &A, const U128 &f, const U128 &g) {
 #if defined(__HIP_DEVICE_COMPILE__)
+    // The same sum as three short chains: bits 0..95 (a0 f0 + g.lo, + a0 f1,
+    // + a1 f0: carries c1 at 2^64, c3 at 2^96), the 2^64 column (g.hi + a0 f2
+    // + a1 f1 + a2 f0) and the 2^96 column's low words (four v_mul_lo), then
+    // two add-with-carry steps.  Ten quarter-rate multiplies as before, but
+    // three deep instead of ten: a fill's state update no longer waits on one
+    // carry chain through every product.
     const uint32_t a0 = (uint32_t)A.lo, a1 = (uint32_t)(A.lo >> 32), a2 = (uint32_t)A.hi, a3 = (uint32_t)(A.hi >> 32);
     const uint32_t f0 = (uint32_t)f.lo, f1 = (uint32_t)(f.lo >> 32), f2 = (uint32_t)f.hi, f3 = (uint32_t)(f.hi >> 32);
-    uint64_t c1, c2, c3, c4, cx;
+    uint64_t c1, c3, k, cx;
     const uint64_t P = mad64c(a0, f0, g.lo, c1);
-    const uint64_t Q = mad64c(a0, f1, (g.hi << 32) | (P >> 32), c2);
+    const uint64_t Q = mad64c(a0, f1, P >> 32, cx);                  // < 2^64: no carry
     const uint64_t R = mad64c(a1, f0, Q, c3);
-    const uint64_t S = mad64c(a0, f2, (g.hi & 0xffffffff00000000ULL) | (R >> 32), cx);
-    const uint64_t T = mad64c(a1, f1, S, cx);
-    const uint64_t U = mad64c(a2, f0, T, cx);
-    const uint32_t r2 = addc32((uint32_t)U, c1, c4);
-    uint64_t W = mad64c(a0, f3, U >> 32, cx);
-    W = mad64c(a1, f2, W, cx);
-    W = mad64c(a2, f1, W, cx);
-    W = mad64c(a3, f0, W, cx);
-    const uint32_t r3 = addc32(addc32(addc32((uint32_t)W, c2, cx), c3, cx), c4, cx);
+    uint64_t S = mad64c(a0, f2, g.hi, cx);                           // carries out of the 2^64 column are >= 2^128
+    S = mad64c(a1, f1, S, cx);
+    const uint64_t U = mad64c(a2, f0, S, cx);
+    const uint32_t w = a0 * f3 + a1 * f2 + a2 * f1 + a3 * f0;
+    const uint32_t r2 = addc32v((uint32_t)U, (uint32_t)(R >> 32), c1, k);
+    const uint32_t r3 = addc32(addc32v((uint32_t)(U >> 32), w, c3, cx), k, cx);
     return U128{(R << 32) | (uint32_t)P, ((uint64_t)r3 << 32) | r2};
 #else
     const unsigned __int128 a = ((unsigned __int128)A.hi << 64) | A.lo, b = ((unsigned __int128)f.hi << 64) | f.lo;
