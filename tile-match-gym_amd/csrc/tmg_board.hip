@@ -1407,13 +1407,15 @@ __device__ __forceinline__ RowPlanes<NB> bp_from_lds(const Params &P, const WS &
 // bounded draw, p = thr / 2^32 per word): g is then back at its starting
 // state and the caller redoes the board on an exact draw-by-draw path.
 // Leaves the board in LDS (colour plane; types 1) and its mask in w.effw.
-template <int NB, class WS>
+// PRIO: the regenerating wave goes first at issue.  A launch that regenerates
+// boards lasts as long as its slowest board, one serial chain of redraws on
+// one wave, while the other streams' steps share its SIMD (measured: the lean
+// kernels' inline autoreset and the 512-cell reset kernel gain; the 128-cell
+// masked reset, beside the c3 step kernels, loses 0.6 %: not raised there).
+template <int NB, bool PRIO = true, class WS>
 __device__ __forceinline__ int bp_generate(const Params &P, WS &w, int lane, Rng &g) {
     const int R = P.R, C = P.C, N = P.N;
-    // A launch that regenerates boards lasts as long as its slowest board, one
-    // serial chain of redraws on one wave, while the other streams' steps
-    // share its SIMD: the regenerating wave goes first at issue
-    __builtin_amdgcn_s_setprio(3);
+    if constexpr (PRIO) __builtin_amdgcn_s_setprio(3);
     // g is wave-uniform; said so explicitly, since where the divergence analysis
     // cannot see it (the lean step kernel's inline autoreset) the ring's
     // counters and state otherwise go to VGPRs and its loops run exec-masked
@@ -1456,7 +1458,7 @@ __device__ __forceinline__ int bp_generate(const Params &P, WS &w, int lane, Rng
         fl = FL_SHUF;
         bp_ring_init<NB>(P, w, lane, g, r, J);
     }
-    __builtin_amdgcn_s_setprio(0);
+    if constexpr (PRIO) __builtin_amdgcn_s_setprio(0);
     if (rej) {
         COVER(CV_REJECT_GEN);
         g = g0;
@@ -2655,7 +2657,7 @@ __device__ __forceinline__ void reset_env(const Params &P, WS &w, int lane, int6
     // wider board takes the exact draw-by-draw path
     int fl = -1;
     if constexpr (SBNB > 0) {
-        if (P.C <= 32) fl = bp_generate<SBNB>(P, w, lane, g);
+        if (P.C <= 32) fl = bp_generate<SBNB, (MAXN > 128)>(P, w, lane, g);
     }
     if (fl < 0) {
         const LaneJump J = load_jump(P, lane, g);
