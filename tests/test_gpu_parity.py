@@ -180,6 +180,9 @@ def test_generate_golden_gpu():
     # position mid-generation (board.py:102-118)
     (9, 15, 15, 0, 2048, 24),
     (10, 14, 14, 0, 2048, 24),
+    # bench.py's generic-shape configs g1 / g2 (no shape-specialised kernel)
+    (10, 10, 5, 0, 4096, 65),
+    (20, 20, 6, 14, 512, 35),
 ])
 def test_oracle_parity_random_actions(cfg):
     """Batched random-action rollouts with autoreset vs the CPU oracle, every step."""
