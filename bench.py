@@ -286,7 +286,7 @@ def main():
             raise SystemExit("--api vector takes the uniform action stream (actions are the caller's)")
         venv = TileMatchVectorEnv(nb, R, C, k, moves, cl, co, device=dev, autoreset_mode="next_step",
                                   obs_dtype=torch.int32 if args.obs_dtype == "int32" else torch.int8,
-                                  action_masks=True, groups=args.groups)
+                                  action_masks=True, groups=args.groups, copy=False)
         venv.vec.set_seed(shard_seeds(rank, nb))
         env = venv.vec
     else:

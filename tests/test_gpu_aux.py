@@ -93,31 +93,48 @@ def test_checkpoint_restore_continues_bit_exact(tmp_path):
             assert torch.equal(getattr(env, f), getattr(env2, f)), (t, f)
 
 
-@pytest.mark.parametrize("cfg", [(8, 8, 3, 14), (10, 10, 4, 0)])
+# (8, 8, 3, 14) / (10, 10, 4, 14): the 128-cell general kernels (deferred
+# resets); (10, 10, 4, 0): the lean c2 kernel (inline); (20, 20, 6, 15): the
+# 512-cell c5 kernels; (7, 9, 5, 15): an odd cell count (2N % 4 == 2, boards
+# not dword-aligned) through the general kernel's same-step final boards.
+@pytest.mark.parametrize("cfg", [(8, 8, 3, 14), (10, 10, 4, 0), (10, 10, 4, 14), (20, 20, 6, 15), (7, 9, 5, 15)])
+@pytest.mark.parametrize("obs_dtype", ["int32", "int8"])
 @pytest.mark.parametrize("groups", [1, 3])
 @pytest.mark.parametrize("mode", ["next_step", "same_step"])
-def test_vector_env_autoreset_modes(mode, groups, cfg):
+def test_vector_env_autoreset_modes(mode, groups, obs_dtype, cfg):
     """TileMatchVectorEnv (gymnasium vector API) vs the oracle driven with the
     same autoreset semantics (tests/vector_ref.py): obs, rewards, terminations,
     infos, action masks, final boards — the general kernels (deferred resets)
-    and the lean ones (inline), on one and on three group streams."""
+    and the lean ones (inline), on one and on three group streams, int32
+    (kernel-written) and int8 (the live state) observations.  copy=True (the
+    default): every returned tensor keeps its value after the next step."""
     from tile_match_gym_amd.vector import TileMatchVectorEnv
     from vector_ref import VectorOracle
     R, C, k, sm = cfg
-    n, moves = 256, 6
+    n, moves = (128 if R * C > 128 else 256), 6
     cl, co = _lists(sm)
-    venv = TileMatchVectorEnv(n, R, C, k, moves, cl, co, seed=40, device=DEV, autoreset_mode=mode, groups=groups)
+    odt = torch.int32 if obs_dtype == "int32" else torch.int8
+    venv = TileMatchVectorEnv(n, R, C, k, moves, cl, co, seed=40, device=DEV, autoreset_mode=mode, groups=groups,
+                              obs_dtype=odt)
     ref = orc.OracleBatch(R, C, k, sm, moves, venv.vec.rng_words().copy())
     obs, info = venv.reset()
     ref.reset()
+    assert obs["board"].dtype == odt
     assert np.array_equal(obs["board"].cpu().numpy(), ref.board.astype(np.int32))
     A = venv.single_action_space.n
     assert venv.action_space.shape == (venv.num_envs,) and (venv.action_space.nvec == A).all()
     vo = VectorOracle(ref, mode)
     rs = np.random.default_rng(1)
+    kept = None
     for t in range(3 * moves + 2):
         a = rs.integers(0, A, n).astype(np.int32)
         obs, rew, term, trunc, info = venv.step(torch.from_numpy(a).to(DEV))
+        if kept is not None:                       # copies of the previous step, untouched by this one
+            for got, want_prev in zip(kept[0], kept[1]):
+                assert np.array_equal(got.cpu().numpy(), want_prev), t
+        kept = ((obs["board"], obs["num_moves_left"], rew, term, info["action_mask"]),
+                tuple(x.cpu().numpy().copy() for x in (obs["board"], obs["num_moves_left"], rew, term,
+                                                       info["action_mask"])))
         want = vo.step(a)
         want_term = want["terminated"][:, 0].astype(bool)
         if mode == "same_step":
@@ -313,3 +330,36 @@ def test_captured_steps_match_eager(cfg, policy):
     if policy:
         assert torch.equal(envs[0].actions, envs[1].actions)
     assert envs[1].status() == 0
+
+
+def test_vecenv_autoreset_mode_survives_toggle_and_checkpoint(tmp_path):
+    """The autoreset mode is one field: toggling the bool keeps next-step mode,
+    and a checkpoint taken in next-step mode restores into next-step mode (its
+    pending resets are implicit in timer == num_moves)."""
+    from tile_match_gym_amd.vec_env import TileMatchVecEnv
+    n, R, C, k, moves = 64, 8, 8, 3, 4
+    env = TileMatchVecEnv(n, R, C, k, moves, [], [], seed=3, device=DEV, autoreset=False)
+    assert env.autoreset_mode == "none" and not env.autoreset
+    env.set_step_outputs("next_step")
+    assert env.autoreset_mode == "next_step" and env.autoreset
+    env.autoreset = True
+    assert env.autoreset_mode == "next_step"
+    env.reset()
+    acts = torch.zeros(n, dtype=torch.int32, device=DEV)
+    for _ in range(moves):
+        env.step_raw(acts)
+    env.join()
+    p = tmp_path / "ck.npz"
+    env.save(p)
+    env2 = TileMatchVecEnv.load(p, device=DEV)
+    assert env2.autoreset_mode == "next_step"
+    env.step_raw(acts)           # every env ended last call: regenerated now, timer 0
+    env2.step_raw(acts)
+    env.join(); env2.join()
+    for f in ("board", "rng", "timer", "eff", "reward", "flags"):
+        assert torch.equal(getattr(env, f), getattr(env2, f)), f
+    assert (env.timer == 0).all()
+    env.autoreset = False
+    assert env.autoreset_mode == "none"
+    env.autoreset = True
+    assert env.autoreset_mode == "same_step"

@@ -19,7 +19,7 @@ def _specials(sm):
     return cl, co
 
 
-@pytest.mark.parametrize("R,C", [(10, 10), (20, 20), (3, 4)])
+@pytest.mark.parametrize("R,C", [(10, 10), (20, 20), (3, 4), (22, 23)])   # W = 3, 12, 1, 16 (the maximum)
 def test_sample_effective_matches_numpy(R, C):
     from tile_match_gym_amd import _native
     ctx = _native.Context(0, R, C, 4, 0, 30)

@@ -36,7 +36,7 @@ class VectorOracle:
         o.step(a, autoreset=False)            # pending envs: step-after-done error, state untouched
         live = ~self.pending if self.mode == "next_step" else np.ones_like(self.pending)
         f = o.flags
-        out = {"terminated": np.stack([(f & 1) != 0, (f & 2) != 0, (f & 4) != 0, (f & 0x80) != 0], 1)
+        out = {"terminated": np.stack([(f & 1) != 0, (f & 2) != 0, (f & 4) != 0, (f & 0xC0) != 0], 1)
                & live[:, None],
                "reward": np.where(live, o.reward, 0), "n_new": np.where(live, o.n_new, 0),
                "n_act": np.where(live, o.n_act, 0)}

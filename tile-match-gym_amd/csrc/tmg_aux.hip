@@ -35,29 +35,55 @@ __global__ __launch_bounds__(256) void onehot_kernel(int64_t n, int N, int k, in
 // — the same stream as shard.synthetic_actions, so any shard layout picks the
 // same actions.  The r-th set bit, r = hi32(h) * count >> 32; with no
 // effective action (a finished env without autoreset) hi32(h) * A >> 32.
-// One thread per env; W <= 16 mask words.  (The step kernel samples the same
-// way in its prologue, sample_action in tmg_board.hip, for tmg_step_groups.)
+// One thread per env; W <= 16 mask words (A < 2 * 512).  (The step kernel
+// samples the same way in its prologue, sample_action in tmg_board.hip, for
+// tmg_step_groups.)
+// The block's 256 mask rows are one contiguous run of 256 W words: the wave
+// loads it coalesced into LDS (rows padded to an odd word count, so the
+// per-thread row reads that follow spread over the banks), then each thread
+// walks its row there.  The r-th set bit of a word is a branch-free binary
+// search on popcounts of its halves (6 steps), not a loop over the set bits.
+constexpr int kSampleMaxW = 16;
+__device__ __forceinline__ int nth_set_bit(uint64_t x, int r) {       // r < popcount(x)
+    int pos = 0;
+#pragma unroll
+    for (int sh = 32; sh > 0; sh >>= 1) {
+        const int c = __popcll(x & ((1ULL << sh) - 1ULL));
+        const bool up = r >= c;
+        r -= up ? c : 0;
+        x = up ? x >> sh : x;
+        pos += up ? sh : 0;
+    }
+    return pos;
+}
 __global__ __launch_bounds__(256) void sample_effective_kernel(int64_t n, int W, int A, const uint64_t *__restrict__ eff,
                                                                uint64_t key, int64_t first_env, int32_t t,
                                                                int32_t *__restrict__ actions) {
-    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    __shared__ uint64_t rows[256 * (kSampleMaxW + 1)];
+    const int64_t base = (int64_t)blockIdx.x * 256;
+    const int64_t i = base + threadIdx.x;
+    const int Wp = W | 1;
+    const int cnt = (int)((n - base) < 256 ? (n - base) : 256);
+    const uint64_t *src = eff + base * W;
+    for (int q = threadIdx.x; q < cnt * W; q += 256) {
+        const int row = q / W;
+        rows[row * Wp + (q - row * W)] = src[q];
+    }
+    __syncthreads();
     if (i >= n) return;
     const uint64_t h = policy_draw(key, (uint64_t)(first_env + i), t);
-    const uint64_t *m = eff + i * W;
+    const uint64_t *m = rows + threadIdx.x * Wp;
     int count = 0;
     for (int j = 0; j < W; j++) count += __popcll(m[j]);
     if (count == 0) { actions[i] = (int32_t)((h * (uint64_t)A) >> 32); return; }
     int r = (int)((h * (uint64_t)count) >> 32);
-    for (int j = 0; j < W; j++) {
-        uint64_t x = m[j];
-        const int c = __popcll(x);
-        if (r < c) {
-            for (; r > 0; r--) x &= x - 1;              // drop the r lowest set bits
-            actions[i] = j * 64 + (__ffsll((unsigned long long)x) - 1);
-            return;
-        }
+    int j = 0;
+    uint64_t x = m[0];
+    for (int c = __popcll(x); r >= c && j < W - 1; c = __popcll(x)) {
         r -= c;
+        x = m[++j];
     }
+    actions[i] = j * 64 + nth_set_bit(x, r);
 }
 
 // utils.compute_num_states / is_valid_state (src/tile_match_gym/utils/utils.py:6-26):

@@ -623,7 +623,8 @@ __device__ __forceinline__ void store_obs(const Params &P, const WS &w, int lane
 __device__ __forceinline__ void store_vo(const Params &P, int64_t e, int flags, int tnew) {
     if (P.vo_term) {
         const uint32_t v = ((flags & FL_DONE) ? 1u : 0u) | ((flags & FL_COMBO) ? 1u << 8 : 0u) |
-                           ((flags & FL_SHUF) ? 1u << 16 : 0u) | ((flags & FL_ERR) ? 1u << 24 : 0u);
+                           ((flags & FL_SHUF) ? 1u << 16 : 0u) |
+                           ((flags & (FL_ERR | FL_OVF)) ? 1u << 24 : 0u);
         reinterpret_cast<uint32_t *>(P.vo_term)[e] = v;
     }
     if (P.vo_left) P.vo_left[e] = (int64_t)(P.num_moves - tnew);
@@ -786,6 +787,212 @@ __device__ __forceinline__ bool scan_effective_clean(const Params &P, WS &w, int
     return any != 0ULL;
 }
 
+// ------------------------------------------ effective-action scan on row bit-planes
+// scan_effective_clean's predicate (and scan_effective's precheck), row-parallel:
+// lane r holds row r of the board as NBV bit-planes of the colour VALUE (bit c
+// of plane b = bit b of the colour of cell (r, c); 0 = colourless or outside
+// the board), so a lane decides the C vertical actions (r, c)-(r+1, c) and the
+// C-1 horizontal actions (r, c)-(r, c+1) of its row at once with 32-bit mask
+// logic, and one pass covers every action of the board (scan_effective_clean:
+// one action per lane and direction, ~14 byte reads each, ceil(A / 128)
+// passes: 2 at 10x10, 6 at 20x20).
+// D(x, y) = columns where two (shifted) rows differ in colour; a pattern of two
+// cells matches the moved colour where the OR of its two D masks is 0, and an
+// action is effective where one of its eight patterns matches (or by type: both
+// swapped tiles special, or one a cookie; board.py:735-787).  Cells outside the
+// board read colour 0, which differs from every coloured tile; a colourless
+// cookie may "match" them, but a swap moving a cookie is effective by type
+// anyway.  D masks moved sideways shift in ones (outside = differ), moved across
+// lanes (DPP wave shifts) lanes off the board read all ones.  Each D mask is
+// computed once and reused by the patterns that look at the same cell pair from
+// the other side (a pair of rows one lane up, a column shift).
+// C <= kRowScanMaxC: the horizontal patterns reach column c + 3 and the shifted
+// masks column C + 1, inside 32 bits.
+constexpr int kRowScanMaxC = 28;
+__host__ __device__ constexpr int rs_planes(int k) { return k < 2 ? 1 : k < 4 ? 2 : k < 8 ? 3 : 4; }
+
+// bit b of each byte of x as 4 bits (byte i -> bit i): the masked bits sit 8
+// apart, so one multiply moves each to bit 28 + i with no carries
+__device__ __forceinline__ uint32_t byte_bits(uint32_t x, int b) {
+    return ((x & (0x01010101u << b)) * (0x10204080u >> b)) >> 28;
+}
+// bit 0 of each byte = OR of that byte's 8 bits (the shifts stay inside the byte for bit 0)
+__device__ __forceinline__ uint32_t byte_any(uint32_t x) {
+    x |= x >> 4;
+    x |= x >> 2;
+    return x | (x >> 1);
+}
+// lane l <- lane l+1 (DPP wave_shl:1; lane 63 <- old) / lane l <- lane l-1 (wave_shr:1; lane 0 <- old)
+__device__ __forceinline__ uint32_t from_next_lane(uint32_t v, uint32_t old) {
+    return (uint32_t)__builtin_amdgcn_update_dpp((int)old, (int)v, 0x130, 0xf, 0xf, false);
+}
+__device__ __forceinline__ uint32_t from_prev_lane(uint32_t v, uint32_t old) {
+    return (uint32_t)__builtin_amdgcn_update_dpp((int)old, (int)v, 0x138, 0xf, 0xf, false);
+}
+// bytes [off, off + 4 nd) of the LDS board (nd <= 8), realigned to dwords
+template <class WS>
+__device__ __forceinline__ void lds_row(const WS &w, int off, int nd, uint32_t (&d)[8]) {
+    const uint32_t *b = reinterpret_cast<const uint32_t *>(w.brd + (off & ~3));
+    const uint32_t sh = (uint32_t)(off & 3) * 8u;
+    uint32_t raw[9];
+#pragma unroll
+    for (int i = 0; i < 9; i++) raw[i] = i <= nd ? b[i] : 0u;
+#pragma unroll
+    for (int i = 0; i < 8; i++) d[i] = i < nd ? __builtin_amdgcn_alignbit(raw[i + 1], raw[i], sh) : 0u;
+}
+
+// Fills w.effw (bit a = action a effective); returns 1 if any action is
+// effective, 0 if none, -1 (clean = false only) when the board is not one the
+// predicate covers — an empty cell, a coloured cookie, a colour outside 0..2^NBV-1
+// or a colour triple — and the caller must run the exact scan.  TYPES = false:
+// every type is 1 (the lean kernels).
+template <bool TYPES, int NBV, class WS>
+__device__ __forceinline__ int scan_rows_nb(const Params &P, WS &w, int lane_, bool clean) {
+    const int R = P.R, C = P.C, N = P.N;
+    const int r = loop_lane(lane_);
+    const bool on = r < R;
+    const int rr = on ? r : 0;
+    const int nd = (C + 3) >> 2;
+    // ---- row r as bit-planes (and, with specials, its special / cookie / empty masks)
+    uint32_t X[NBV];
+    bool odd = false;
+    {
+        uint32_t d[8];
+        lds_row(w, rr * C, nd, d);
+#pragma unroll
+        for (int b = 0; b < NBV; b++) X[b] = 0u;
+        uint32_t hi = 0u;
+#pragma unroll
+        for (int j = 0; j < 8; j++) {
+            if (j < nd) {
+#pragma unroll
+                for (int b = 0; b < NBV; b++) X[b] |= byte_bits(d[j], b) << (4 * j);
+                hi |= d[j];
+            }
+        }
+        // a colour with bits above the planes (a hand-edited board) would alias
+        if (!clean) odd = (hi & (0x01010101u * (0xFFu & (0xFFu << NBV)))) != 0u;
+    }
+    const uint32_t cm = on ? (C >= 32 ? ~0u : (1u << C) - 1u) : 0u;    // the row's columns
+#pragma unroll
+    for (int b = 0; b < NBV; b++) X[b] &= cm;
+    uint32_t NS = 0u, CK = 0u, Z = 0u;             // type not in {0, 1} / cookie (type < 0) / empty (type 0)
+    if constexpr (TYPES) {
+        uint32_t d[8];
+        lds_row(w, N + rr * C, nd, d);
+#pragma unroll
+        for (int j = 0; j < 8; j++) {
+            if (j < nd) {
+                NS |= byte_bits(byte_any(d[j] & 0xFEFEFEFEu), 0) << (4 * j);
+                CK |= byte_bits(d[j] >> 7, 0) << (4 * j);
+                if (!clean) Z |= byte_bits(~byte_any(d[j]), 0) << (4 * j);
+            }
+        }
+        NS &= cm; CK &= cm; Z &= cm;
+    }
+    // ---- rows r+1 .. r+3 (lanes off the board hold 0: colour 0 = outside)
+    uint32_t X1[NBV], X2[NBV], X3[NBV];
+#pragma unroll
+    for (int b = 0; b < NBV; b++) {
+        X1[b] = from_next_lane(X[b], 0u);
+        X2[b] = from_next_lane(X1[b], 0u);
+        X3[b] = from_next_lane(X2[b], 0u);
+    }
+    const auto D = [&](const uint32_t (&x)[NBV], int sx, const uint32_t (&y)[NBV], int sy) -> uint32_t {
+        uint32_t m = 0u;      // columns c where colour(x row, c + sx) != colour(y row, c + sy)
+#pragma unroll
+        for (int b = 0; b < NBV; b++) {
+            const uint32_t xs = sx >= 0 ? x[b] >> sx : x[b] << -sx;
+            const uint32_t ys = sy >= 0 ? y[b] >> sy : y[b] << -sy;
+            m |= xs ^ ys;
+        }
+        return m;
+    };
+    // the D masks (bit c: the two cells named differ)
+    const uint32_t E1 = D(X1, -1, X, 0);      // (r+1, c-1) vs (r, c)
+    const uint32_t E2 = D(X1, -2, X, 0);      // (r+1, c-2) vs (r, c)
+    const uint32_t F1 = D(X1, 1, X, 0);       // (r+1, c+1) vs (r, c)
+    const uint32_t F2 = D(X1, 2, X, 0);       // (r+1, c+2) vs (r, c)
+    const uint32_t V2d = D(X2, 0, X, 0);      // (r+2, c) vs (r, c)
+    const uint32_t V3d = D(X3, 0, X, 0);      // (r+3, c) vs (r, c)
+    const uint32_t G2 = D(X, 2, X, 0);        // (r, c+2) vs (r, c)
+    const uint32_t G3 = D(X, 3, X, 0);        // (r, c+3) vs (r, c)
+    const uint32_t W2 = D(X2, 1, X, 0);       // (r+2, c+1) vs (r, c)
+    const uint32_t Dn2 = D(X2, 0, X, 1);      // (r+2, c) vs (r, c+1)
+    // the same pairs seen from lanes above (off the board: all ones = differ)
+    const uint32_t A = from_prev_lane(V2d, ~0u);                       // (r-1, c) vs (r+1, c)
+    const uint32_t B = from_prev_lane(from_prev_lane(V3d, ~0u), ~0u);  // (r-2, c) vs (r+1, c)
+    const uint32_t U1 = from_prev_lane(F1, ~0u);                       // (r-1, c) vs (r, c+1)
+    const uint32_t U2 = from_prev_lane(from_prev_lane(W2, ~0u), ~0u);  // (r-2, c) vs (r, c+1)
+    const uint32_t V1 = from_prev_lane(E1, ~0u) >> 1;                  // (r-1, c+1) vs (r, c)
+    const uint32_t V2 = from_prev_lane(from_prev_lane(Dn2, ~0u), ~0u); // (r-2, c+1) vs (r, c)
+    // vertical action (r, c): p = (r, c) takes x2 = colour(r+1, c), q = (r+1, c) takes x1 = colour(r, c)
+    const uint32_t F1l = (F1 << 1) | 1u, F2l = (F2 << 2) | 3u;         // (r, c-1) / (r, c-2) vs (r+1, c)
+    const uint32_t E1r = E1 >> 1, E2r = E2 >> 2;                       // (r, c+1) / (r, c+2) vs (r+1, c)
+    const uint32_t nv_ = (A | B) & (F1l | F2l) & (F1l | E1r) & (E1r | E2r)     // p: up-up, left-left, left-right, right-right
+                       & (V2d | V3d) & (E1 | E2) & (E1 | F1) & (F1 | F2);      // q: down-down, left-left, left-right, right-right
+    // horizontal action (r, c): p = (r, c) takes x2 = colour(r, c+1), q = (r, c+1) takes x1 = colour(r, c)
+    const uint32_t G2l = (G2 << 1) | 1u, G3l = (G3 << 2) | 3u;         // (r, c-1) / (r, c-2) vs (r, c+1)
+    const uint32_t Dn1 = E1 >> 1;                                      // (r+1, c) vs (r, c+1)
+    const uint32_t nh_ = (G2l | G3l) & (U1 | U2) & (U1 | Dn1) & (Dn1 | Dn2)    // p: left-left, up-up, up-down, down-down
+                       & (G2 | G3) & (V1 | V2) & (V1 | F1) & (F1 | W2);        // q: right-right, up-up, up-down, down-down
+    uint32_t tv = 0u, th = 0u;                 // effective by type
+    if constexpr (TYPES) {
+        const uint32_t NS1 = from_next_lane(NS, 0u), CK1 = from_next_lane(CK, 0u);
+        tv = (NS & NS1) | CK | CK1;
+        th = (NS & (NS >> 1)) | CK | (CK >> 1);
+    }
+    const uint32_t mv = (~nv_ | tv) & (r < R - 1 ? cm : 0u);
+    const uint32_t mh = (~nh_ | th) & (cm >> 1);
+    if (!clean) {
+        // scan_effective's precheck: an empty cell, a coloured cookie, or a
+        // triple (c, c+1, c+2) / (r, r+1, r+2) whose third cell is not a cookie
+        uint32_t nz = 0u;
+#pragma unroll
+        for (int b = 0; b < NBV; b++) nz |= X[b];
+        const uint32_t G1 = D(X, 1, X, 0), V1d = D(X1, 0, X, 0);
+        const uint32_t CK2 = from_next_lane(from_next_lane(CK, 0u), 0u);
+        const uint32_t th3 = ~(G1 | G2) & ~(CK >> 2) & (cm >> 2);
+        const uint32_t tv3 = ~(V1d | V2d) & ~CK2 & (r < R - 2 ? cm : 0u);
+        odd |= (Z | (CK & nz) | th3 | tv3) != 0u;
+        if (__ballot(odd) != 0ULL) return -1;
+    }
+    // the rows' masks into w.effw: bit r*C + c (vertical), nv + r*(C-1) + c (horizontal)
+    if (lane_ < P.W) w.effw[lane_] = 0ULL;
+    WFENCE();
+    const auto put = [&](uint32_t m, int pos) {
+        const int wi = pos >> 6, sh = pos & 63;
+        if (m) {
+            atomicOr(reinterpret_cast<unsigned long long *>(&w.effw[wi]), (unsigned long long)m << sh);
+            const uint64_t up = sh > 32 ? (uint64_t)m >> (64 - sh) : 0ULL;
+            if (up) atomicOr(reinterpret_cast<unsigned long long *>(&w.effw[wi + 1]), (unsigned long long)up);
+        }
+    };
+    put(mv, rr * C);
+    put(mh, C * (R - 1) + rr * (C - 1));
+    WFENCE();
+    return __ballot((mv | mh) != 0u) != 0ULL ? 1 : 0;
+}
+
+// scan_rows_nb for the env's colour count (one instantiation survives in the
+// shape-specialised kernels)
+template <bool TYPES, class WS>
+__device__ __forceinline__ int scan_rows(const Params &P, WS &w, int lane, bool clean) {
+    switch (rs_planes(P.k)) {
+    case 1: return scan_rows_nb<TYPES, 1>(P, w, lane, clean);
+    case 2: return scan_rows_nb<TYPES, 2>(P, w, lane, clean);
+    case 3: return scan_rows_nb<TYPES, 3>(P, w, lane, clean);
+    default: return scan_rows_nb<TYPES, 4>(P, w, lane, clean);
+    }
+}
+
+// Where the row-plane scan replaces the per-action one (A/B switch, bits):
+// 1 = scan_effective (general kernels, hand-edited boards), 2 = the lean /
+// scalar-bitboard ensure loop (sb_ensure), 4 = bp_generate's possible_move.
+#ifndef TMG_RSCAN
+#define TMG_RSCAN 7
+#endif
+
 // _get_effective_actions / possible_move (tile_match_env.py:118-124, board.py:558-569):
 // fills w.effw, returns whether any action is effective.  `clean` = the caller
 // knows the board has no cookie and no colour triple (it just came out of a
@@ -795,7 +1002,11 @@ __device__ __forceinline__ bool scan_effective(const Params &P, WS &w, int lane,
     const int R = P.R, C = P.C, N = P.N;
     const int8_t *col = w.brd, *typ = w.brd + N;
     bool exact = false;
-    if (!clean) {
+    if ((TMG_RSCAN & 1) && C <= kRowScanMaxC) {
+        const int r = scan_rows<true>(P, w, lane, clean);         // its own precheck
+        if (r >= 0) return r != 0;
+        exact = true;
+    } else if (!clean) {
         // an empty cell, a cookie that gained a colour or a pre-existing triple ->
         // exact scan.  Colourless cookies are fine: swapping one is effective
         // (board.py:752-753), and colour 0 matches no coloured tile; a cookie
@@ -1277,10 +1488,18 @@ __device__ __forceinline__ bool bp_rejected(const Params &P, const BpRing &r) {
 // batch, m = (fill >> 7) - (i >> 7) batches after i's (1 <= m <= 6: the
 // redraw loop keeps fewer than N + 128 <= 640 colours filled ahead), so s = A^{-64m} X - A^{-64m}
 // G_{64m} inc (jump-table row 63 + m).
+// Colours filled ahead of the consume position: bp_prefetch fills while fewer
+// than maxM <= N <= 512 (C <= 32, N <= 512) are ahead, 128 at a time.
+constexpr int kBpMaxAhead = 512 + 128;
+static_assert(kBpMaxAhead / 128 + 1 <= kJumpRows - 64,
+              "bp_ring_state's backward jump needs a jump-table row for every batch count the ring can reach");
 __device__ __forceinline__ void bp_ring_state(const Params &P, const BpJump &J, const BpRing &r, Rng &g) {
     if (r.cons == r.cons0) return;                                   // nothing taken since bp_ring_init(g)
     const int i = r.cons - 1, local = i & 127;                       // i >= 128: a take draws >= 2 colours
     const int m = __builtin_amdgcn_readfirstlane((r.fill >> 7) - (i >> 7));
+#if TMG_COVER
+    if (m < 1 || m > kJumpRows - 64) P.status[0] = 1u;              // (m wave-uniform) the table has no such row
+#endif
     const int l = bp_lane(local >> 1);
     const U128 x{rdlane64(J.X.lo, l), rdlane64(J.X.hi, l)};
     const uint64_t *t = P.jump + (63 + m) * 4;
@@ -1448,7 +1667,9 @@ __device__ __forceinline__ int bp_generate(const Params &P, WS &w, int lane, Rng
         if ((rej = bp_rejected(P, r))) break;
         bp_to_lds<NB>(P, w, lane, pl);
         WSYNC();
-        if (scan_effective_clean<false>(P, w, lane)) break;             // possible_move, :102
+        if ((TMG_RSCAN & 4) && P.C <= kRowScanMaxC ? scan_rows<false>(P, w, lane, true) != 0
+                                                    : scan_effective_clean<false>(P, w, lane))
+            break;                                                       // possible_move, :102
         if (shuffles >= kMaxShuffles) { fl = FL_ERR; break; }
         COVER(CV_SHUFFLE_GEN);
         bp_ring_state(P, J, r, g);                                       // shuffle draws from the stream itself
@@ -2345,6 +2566,31 @@ __device__ __forceinline__ uint32_t step_env(
         a = __builtin_amdgcn_readfirstlane(sample_action(P, effrow, e, lane));
         if (lane == 0) const_cast<int32_t *>(actions)[e] = a;
     }
+    // The common ineffective move (board.py:352-353; ~76 % of uniform moves at
+    // c2): a live env, a trusted mask, not the episode's last move — only the
+    // timer and the zero outputs are written.  Tested ahead of everything else
+    // with as little wave-uniform logic as possible (the autoreset mode, the
+    // board / mask addresses and the rare outputs stay in the general path
+    // below), and the per-env arrays are addressed by the VALU (SGPR base +
+    // an opaque 64-bit VGPR index, one v_lshl_add each) instead of a 64-bit
+    // SALU add pair per array: the scalar unit is the c2 kernel's busiest pipe.
+#ifndef TMG_QEXIT
+#define TMG_QEXIT 1
+#endif
+    if (TMG_QEXIT && trust_eff && t0 < P.num_moves - 1 && (unsigned)a < (unsigned)P.A) {
+        if (!((rdlane64(effrow, a >> 6) >> (a & 63)) & 1ULL)) {
+            if (lane == 0) {
+                uint64_t ve = (uint64_t)e;
+                TMG_OPAQUE_V(ve);
+                timer[ve] = t0 + 1;
+                reward[ve] = 0; n_new[ve] = 0; n_act[ve] = 0;
+                flags_out[ve] = (uint8_t)0;
+                if (P.vo_term) reinterpret_cast<uint32_t *>(P.vo_term)[ve] = 0u;
+                if (P.vo_left) P.vo_left[ve] = (int64_t)(P.num_moves - 1 - t0);
+            }
+            return 0;
+        }
+    }
     // an env that ended last call, with next-step autoreset: reset() now
     // (tested only inside the rare branch, so that the common path carries
     // no extra condition into the ineffective-move exit)
@@ -2383,7 +2629,9 @@ __device__ __forceinline__ uint32_t step_env(
             if (P.vo_mask) store_mask(P, w, lane, e, true);
         }
         if (done && same && P.vo_final) {                                   // the last board, as it stands
-            const int nbw = (2 * N) >> 2;
+            // dwords only when every env's board starts on a dword ((2N) % 4 == 0,
+            // as `bwhole` below); an odd N gives 2-byte-aligned boards: bytes
+            const int nbw = ((2 * N) & 3) == 0 ? (2 * N) >> 2 : 0;
             const uint32_t *src = reinterpret_cast<const uint32_t *>(gb);
             uint32_t *dst = reinterpret_cast<uint32_t *>(P.vo_final + e * 2 * N);
             for (int i = lane; i < nbw; i += 64) dst[i] = src[i];

@@ -586,7 +586,10 @@ int tmg_plan_step(tmg_plan *p, int32_t *actions, int32_t t, int trust_eff, int f
         P.pol_first = p->first_env + lo;
         P.pol_t = t;
         const hipStream_t gs = p->streams[g] ? p->streams[g] : cur;
-        if (P.sample && !(ctx->P.smask == 0 && trust_eff)) {
+#ifndef TMG_GEN_SAMPLE
+#define TMG_GEN_SAMPLE 0
+#endif
+        if (P.sample && !TMG_GEN_SAMPLE && !(ctx->P.smask == 0 && trust_eff)) {
             // the general kernels (low occupancy, long waves) take the draw
             // from the sampler kernel ahead of them; the lean ones sample in
             // their own prologue

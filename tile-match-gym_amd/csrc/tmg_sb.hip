@@ -413,7 +413,9 @@ __device__ __forceinline__ int sb_ensure(const Params &P, WS &w, int lane, const
             WSYNC();
             dirty = false;
         }
-        if (scan_effective_clean<false>(P, w, lane)) break;   // types all 1, no line
+        if ((TMG_RSCAN & 2) && P.C <= kRowScanMaxC ? scan_rows<false>(P, w, lane, true) != 0
+                                                    : scan_effective_clean<false>(P, w, lane))
+            break;                                           // types all 1, no line
         if (shuffles >= kMaxShuffles) { fl |= FL_ERR; break; }
         COVER(GEN ? CV_SHUFFLE_GEN : CV_SHUFFLE);
         WSYNC();

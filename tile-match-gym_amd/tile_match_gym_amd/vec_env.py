@@ -80,7 +80,9 @@ class TileMatchVecEnv:
         self.colourless_specials = list(colourless_specials)
         self.colour_specials = list(colour_specials)
         self.specials_mask = _native.specials_mask(colourless_specials, colour_specials)
-        self._autoreset = bool(autoreset)
+        # the one source of truth for the autoreset semantics: "none",
+        # "same_step" or "next_step" (set_step_outputs); `autoreset` derives from it
+        self._autoreset_mode = "same_step" if autoreset else "none"
         # lib_path: another build of libtmg.so (a diagnostic variant) for this env's context
         self.ctx = _native.Context(device.index if device.index is not None else torch.cuda.current_device(),
                                    num_rows, num_cols, num_colours, self.specials_mask, num_moves, lib_path=lib_path)
@@ -118,7 +120,6 @@ class TileMatchVecEnv:
                                          _ptr(self.eff), bounds, streams) for pol in (False, True)}
         self._policy = (12345, 0)                   # (key, first_env) the policy plan is configured with
         self._vout = {}                             # extra outputs (set_step_outputs)
-        self._autoreset_mode = "same_step" if self.autoreset else "none"
         self._held = []                             # action tensors the queued steps still read
         self._dev_index = device.index if device.index is not None else torch.cuda.current_device()
         self._configure()
@@ -126,17 +127,22 @@ class TileMatchVecEnv:
     # ----------------------------------------------------------------- API
     @property
     def autoreset(self) -> bool:
-        """Same-step autoreset of the envs whose episode ends (settable: the step
-        plans are reconfigured)."""
-        return self._autoreset
+        """Whether envs whose episode ends are reset (same step or, after
+        set_step_outputs("next_step"), the next one).  Settable: True keeps a
+        next-step mode and otherwise selects same-step; False selects none (the
+        step plans are reconfigured)."""
+        return self._autoreset_mode != "none"
+
+    @property
+    def autoreset_mode(self) -> str:
+        return self._autoreset_mode
 
     @autoreset.setter
     def autoreset(self, value):
-        value = bool(value)
-        if value != self._autoreset:
-            self._autoreset = value
+        mode = ("next_step" if self._autoreset_mode == "next_step" else "same_step") if value else "none"
+        if mode != self._autoreset_mode:
             self.join()
-            self._autoreset_mode = "same_step" if value else "none"
+            self._autoreset_mode = mode
             self._configure()
 
     def _stream(self):
@@ -161,6 +167,8 @@ class TileMatchVecEnv:
         autoreset_mode: "none", "same_step", "next_step"."""
         self.join()
         if autoreset_mode is not None:
+            if autoreset_mode not in ("none", "same_step", "next_step"):
+                raise ValueError("autoreset_mode must be 'none', 'same_step' or 'next_step'")
             self._autoreset_mode = autoreset_mode
         self._vout = {k: _ptr(v) for k, v in (("terminated", terminated), ("action_mask", action_mask),
                                                ("moves_left", moves_left), ("final_board", final_board),
@@ -391,7 +399,8 @@ class TileMatchVecEnv:
     def config(self) -> dict:
         return {"num_rows": self.num_rows, "num_cols": self.num_cols, "num_colours": self.num_colours,
                 "num_moves": self.num_moves, "colourless_specials": self.colourless_specials,
-                "colour_specials": self.colour_specials, "num_envs": self.num_envs, "autoreset": self.autoreset}
+                "colour_specials": self.colour_specials, "num_envs": self.num_envs, "autoreset": self.autoreset,
+                "autoreset_mode": self._autoreset_mode}
 
     def state_dict(self) -> dict:
         """Host copy of the whole batched state: boards, the exact PCG64 stream
@@ -431,6 +440,12 @@ class TileMatchVecEnv:
         env = cls(cfg["num_envs"], cfg["num_rows"], cfg["num_cols"], cfg["num_colours"], cfg["num_moves"],
                   cfg["colourless_specials"], cfg["colour_specials"], seeds=range(cfg["num_envs"]), device=device,
                   autoreset=cfg["autoreset"])
+        # next-step mode: the pending resets are implicit in timer == num_moves,
+        # so the mode must come back with the state (older checkpoints: the bool)
+        mode = cfg.get("autoreset_mode")
+        if mode is not None and mode != env._autoreset_mode:
+            env._autoreset_mode = mode
+            env._configure()
         env.load_state_dict(dict(arrays, config=cfg, eff_valid=cfg.get("eff_valid", True)))
         return env
 

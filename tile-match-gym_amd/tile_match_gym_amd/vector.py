@@ -28,9 +28,9 @@ One host call per step (a tmg_plan step over the env groups' streams): the
 kernels themselves reset the envs due (next-step mode), keep the (N, A) mask
 bytes of the envs whose mask changed, and write the terminated / info bytes,
 moves left, the int32 observation boards and (same-step mode) the final
-boards.  The returned tensors are
-views of the env's live buffers, overwritten by the next call; pass
-``copy=True`` for fresh tensors (gymnasium's vector-env ``copy`` flag).
+boards.  As in gymnasium (its vector envs' ``copy`` flag, default True) the
+returned tensors are fresh copies; ``copy=False`` returns views of the env's
+live buffers instead, overwritten by the next call (the benchmark's setting).
 """
 from __future__ import annotations
 
@@ -48,7 +48,7 @@ class TileMatchVectorEnv:
     def __init__(self, num_envs: int, num_rows: int, num_cols: int, num_colours: int, num_moves: int,
                  colourless_specials=(), colour_specials=(), seed: int = 0, device=None,
                  autoreset_mode: str = "next_step", obs_dtype=torch.int32, action_masks: bool = True,
-                 groups: int = 1, copy: bool = False):
+                 groups: int = 1, copy: bool = True):
         if autoreset_mode not in ("next_step", "same_step"):
             raise ValueError("autoreset_mode must be 'next_step' or 'same_step'")
         if obs_dtype not in (torch.int32, torch.int8):
@@ -142,17 +142,18 @@ class TileMatchVectorEnv:
         tb = self._term.view(torch.bool)
         infos = {}
         if self.autoreset_mode == "same_step":
-            infos["final_obs"] = {"board": self._board(self._final), "num_moves_left": self._zero_left}
+            infos["final_obs"] = {"board": self._board(self._final), "num_moves_left": self._c(self._zero_left)}
             infos["_final_obs"] = self._c(tb[:, 0])
         infos["is_combination_match"] = self._c(tb[:, 1])
         infos["num_new_specials"] = self._c(v.n_new)
         infos["num_specials_activated"] = self._c(v.n_act)
         infos["shuffled"] = self._c(tb[:, 2])
-        # a live env whose step met an internal error (never expected)
+        # a live env whose step met an internal error or ran out of list
+        # capacity (byte 3: TMG_FLAG_ERROR | TMG_FLAG_OVERFLOW; never expected)
         infos["error"] = self._c(tb[:, 3])
         if self.action_masks:
             infos["action_mask"] = self._c(self._mask.view(torch.bool))
-        return self._obs(), self._c(v.reward), self._c(tb[:, 0]), self._trunc, infos
+        return self._obs(), self._c(v.reward), self._c(tb[:, 0]), self._c(self._trunc), infos
 
     def close(self):
         self.vec.close()

@@ -66,6 +66,8 @@ inline unsigned max(unsigned a, unsigned b) { return a > b ? a : b; }
 inline uint64_t __builtin_amdgcn_s_memrealtime() { return 0; }
 inline unsigned atomicAdd(unsigned *p, unsigned v) { unsigned o = *p; *p += v; return o; }
 inline unsigned long long atomicAdd(unsigned long long *p, unsigned long long v) { unsigned long long o = *p; *p += v; return o; }
+// lanes run one at a time between collectives, so a plain read-modify-write is the atomic
+inline unsigned long long atomicOr(unsigned long long *p, unsigned long long v) { unsigned long long o = *p; *p |= v; return o; }
 inline void __threadfence() {}
 
 inline unsigned emu_mbcnt_lo(unsigned m, unsigned acc) {
