@@ -56,23 +56,35 @@ __device__ __forceinline__ int nth_set_bit(uint64_t x, int r) {       // r < pop
     }
     return pos;
 }
-__global__ __launch_bounds__(256) void sample_effective_kernel(int64_t n, int W, int A, const uint64_t *__restrict__ eff,
-                                                               uint64_t key, int64_t first_env, int32_t t,
-                                                               int32_t *__restrict__ actions) {
-    __shared__ uint64_t rows[256 * (kSampleMaxW + 1)];
-    const int64_t base = (int64_t)blockIdx.x * 256;
+#ifndef TMG_SAMPLE_BS
+#define TMG_SAMPLE_BS 64
+#endif
+#ifndef TMG_SAMPLE_LDS
+#define TMG_SAMPLE_LDS 0
+#endif
+template <int BS, bool STAGE>
+__global__ __launch_bounds__(BS) void sample_effective_kernel(int64_t n, int W, int A, const uint64_t *__restrict__ eff,
+                                                              uint64_t key, int64_t first_env, int32_t t,
+                                                              int32_t *__restrict__ actions) {
+    __shared__ uint64_t rows[STAGE ? BS * (kSampleMaxW + 1) : 1];
+    const int64_t base = (int64_t)blockIdx.x * BS;
     const int64_t i = base + threadIdx.x;
-    const int Wp = W | 1;
-    const int cnt = (int)((n - base) < 256 ? (n - base) : 256);
-    const uint64_t *src = eff + base * W;
-    for (int q = threadIdx.x; q < cnt * W; q += 256) {
-        const int row = q / W;
-        rows[row * Wp + (q - row * W)] = src[q];
+    const uint64_t *m;
+    if constexpr (STAGE) {
+        const int Wp = W | 1;
+        const int cnt = (int)((n - base) < BS ? (n - base) : BS);
+        const uint64_t *src = eff + base * W;
+        for (int q = threadIdx.x; q < cnt * W; q += BS) {
+            const int row = q / W;
+            rows[row * Wp + (q - row * W)] = src[q];
+        }
+        __syncthreads();
+        m = rows + threadIdx.x * Wp;
+    } else {
+        m = eff + (i < n ? i : 0) * W;
     }
-    __syncthreads();
     if (i >= n) return;
     const uint64_t h = policy_draw(key, (uint64_t)(first_env + i), t);
-    const uint64_t *m = rows + threadIdx.x * Wp;
     int count = 0;
     for (int j = 0; j < W; j++) count += __popcll(m[j]);
     if (count == 0) { actions[i] = (int32_t)((h * (uint64_t)A) >> 32); return; }

@@ -32,8 +32,14 @@ namespace tmg {
 // kernel; each measured on the MI355X against its neighbours.
 constexpr int kLean128Waves = 7;     // step_kernel<128, false>: the c2 / c4 kernel (72 VGPRs; 8: 64, 1 % slower)
 constexpr int kGen128Waves = 5;      // step_kernel<128, true>: c3 (96 VGPRs; 6 / 7 spill and lose, also specialised)
-constexpr int kReset512Waves = 8;    // reset_kernel<512>: c5's regeneration (7: 0.8 % slower, profiles/r04/s7)
-constexpr int kReset128Waves = 8;    // reset_kernel<128> specialised for 10x10 k4 (c3): 63 VGPRs
+#ifndef TMG_RESET512_WAVES
+#define TMG_RESET512_WAVES 8
+#endif
+#ifndef TMG_RESET128_WAVES
+#define TMG_RESET128_WAVES 8
+#endif
+constexpr int kReset512Waves = TMG_RESET512_WAVES;   // reset_kernel<512>: c5's regeneration (7: 0.8 % slower, profiles/r04/s7)
+constexpr int kReset128Waves = TMG_RESET128_WAVES;   // reset_kernel<128> specialised for 10x10 k4 (c3): 63 VGPRs
 // envs per wave of a masked reset_kernel launch (the deferred autoreset after a
 // general step; 29 of 30 find no finished env).  10x10 boards: 1 / 2 / 4 / 8 /
 // 16 measured c3 6.97 / 7.10 / 7.19 / 7.17 / 7.15 x 10^8; 20x20 boards, whose
@@ -653,7 +659,18 @@ __host__ __device__ __forceinline__ uint64_t policy_draw(uint64_t key, uint64_t 
 // a handful of VALU and one ballot instead of a scalar binary search (the
 // scalar unit is the step kernels' busiest pipe).
 __device__ __forceinline__ int sample_action(const Params &P, uint64_t effrow, int64_t e, int lane) {
+#ifndef TMG_DRAW_VALU
+#define TMG_DRAW_VALU 0
+#endif
+#if TMG_DRAW_VALU
+    // the counter hash on the VALU (an opaque lane value), read back once: the
+    // scalar unit is the busiest pipe of an effective step
+    uint64_t gid = (uint64_t)(P.pol_first + e);
+    TMG_OPAQUE_V(gid);
+    const uint32_t h = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)policy_draw(P.pol_key, gid, P.pol_t));
+#else
     const uint32_t h = (uint32_t)policy_draw(P.pol_key, (uint64_t)(P.pol_first + e), P.pol_t);
+#endif
     const int W = P.W;
     const int pc = __popcll(effrow);                    // 0 on lanes >= W
     int count = 0;

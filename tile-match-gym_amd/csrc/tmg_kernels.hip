@@ -151,8 +151,10 @@ void launch_onehot(hipStream_t s, int64_t n, int N, int k, int nsel, int4 sel, c
 }
 void launch_sample_effective(hipStream_t s, int64_t n, int W, int A, const uint64_t *eff, uint64_t key,
                              int64_t first_env, int32_t t, int32_t *actions) {
-    const dim3 grid((unsigned)((n + 255) / 256)), block(256);
-    hipLaunchKernelGGL(sample_effective_kernel, grid, block, 0, s, n, W, A, eff, key, first_env, t, actions);
+    constexpr int BS = TMG_SAMPLE_BS;
+    const dim3 grid((unsigned)((n + BS - 1) / BS)), block(BS);
+    hipLaunchKernelGGL((sample_effective_kernel<BS, TMG_SAMPLE_LDS != 0>), grid, block, 0, s, n, W, A, eff, key,
+                       first_env, t, actions);
 }
 void launch_count_states(int R, int C, int k, uint64_t total, uint64_t per, uint64_t threads,
                          unsigned long long *counts) {
