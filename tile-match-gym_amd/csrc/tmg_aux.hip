@@ -35,27 +35,16 @@ __global__ __launch_bounds__(256) void onehot_kernel(int64_t n, int N, int k, in
 // — the same stream as shard.synthetic_actions, so any shard layout picks the
 // same actions.  The r-th set bit, r = hi32(h) * count >> 32; with no
 // effective action (a finished env without autoreset) hi32(h) * A >> 32.
-// One thread per env; W <= 16 mask words (A < 2 * 512).  (The step kernel
-// samples the same way in its prologue, sample_action in tmg_board.hip, for
-// tmg_step_groups.)
-// The block's 256 mask rows are one contiguous run of 256 W words: the wave
-// loads it coalesced into LDS (rows padded to an odd word count, so the
-// per-thread row reads that follow spread over the banks), then each thread
-// walks its row there.  The r-th set bit of a word is a branch-free binary
-// search on popcounts of its halves (6 steps), not a loop over the set bits.
+// One thread per env; W <= 16 mask words (A < 2 * 512); draw_row
+// (tmg_board.hip) picks the r-th set bit by a branch-free binary search on
+// popcounts.  The lean step kernels sample the same way in their prologue
+// (sample_action); the general ones take this kernel's draw.
+// One-wave workgroups: the launch sits between the group's step launches
+// while the other streams' step waves fill the CUs, and a 64-thread block
+// gets a slot sooner than a 256-thread one (c3-eff 2.37 vs 2.32 x 10^8,
+// profiles/r06/s4).  Staging the block's mask rows through LDS for coalesced
+// loads (STAGE) measured the same (2.36) and stays a template option.
 constexpr int kSampleMaxW = 16;
-__device__ __forceinline__ int nth_set_bit(uint64_t x, int r) {       // r < popcount(x)
-    int pos = 0;
-#pragma unroll
-    for (int sh = 32; sh > 0; sh >>= 1) {
-        const int c = __popcll(x & ((1ULL << sh) - 1ULL));
-        const bool up = r >= c;
-        r -= up ? c : 0;
-        x = up ? x >> sh : x;
-        pos += up ? sh : 0;
-    }
-    return pos;
-}
 #ifndef TMG_SAMPLE_BS
 #define TMG_SAMPLE_BS 64
 #endif
@@ -84,18 +73,7 @@ __global__ __launch_bounds__(BS) void sample_effective_kernel(int64_t n, int W, 
         m = eff + (i < n ? i : 0) * W;
     }
     if (i >= n) return;
-    const uint64_t h = policy_draw(key, (uint64_t)(first_env + i), t);
-    int count = 0;
-    for (int j = 0; j < W; j++) count += __popcll(m[j]);
-    if (count == 0) { actions[i] = (int32_t)((h * (uint64_t)A) >> 32); return; }
-    int r = (int)((h * (uint64_t)count) >> 32);
-    int j = 0;
-    uint64_t x = m[0];
-    for (int c = __popcll(x); r >= c && j < W - 1; c = __popcll(x)) {
-        r -= c;
-        x = m[++j];
-    }
-    actions[i] = j * 64 + nth_set_bit(x, r);
+    actions[i] = draw_row(m, W, A, policy_draw(key, (uint64_t)(first_env + i), t));
 }
 
 // utils.compute_num_states / is_valid_state (src/tile_match_gym/utils/utils.py:6-26):

@@ -688,6 +688,35 @@ __device__ __forceinline__ int sample_action(const Params &P, uint64_t effrow, i
     return j * 64 + __ffsll((unsigned long long)__ballot(hit)) - 1;
 }
 
+// The r-th set bit of x (r < popcount(x)): a branch-free binary search on the
+// popcounts of its halves, 6 steps (not a loop over the set bits)
+__device__ __forceinline__ int nth_set_bit(uint64_t x, int r) {
+    int pos = 0;
+#pragma unroll
+    for (int sh = 32; sh > 0; sh >>= 1) {
+        const int c = __popcll(x & ((1ULL << sh) - 1ULL));
+        const bool up = r >= c;
+        r -= up ? c : 0;
+        x = up ? x >> sh : x;
+        pos += up ? sh : 0;
+    }
+    return pos;
+}
+// tmg_sample_effective's draw for one env by one lane: m = the env's W mask words
+__device__ __forceinline__ int32_t draw_row(const uint64_t *m, int W, int A, uint64_t h) {
+    int count = 0;
+    for (int j = 0; j < W; j++) count += __popcll(m[j]);
+    if (count == 0) return (int32_t)((h * (uint64_t)A) >> 32);
+    int r = (int)((h * (uint64_t)count) >> 32);
+    int j = 0;
+    uint64_t x = m[0];
+    for (int c = __popcll(x); r >= c && j < W - 1; c = __popcll(x)) {
+        r -= c;
+        x = m[++j];
+    }
+    return j * 64 + nth_set_bit(x, r);
+}
+
 // is_move_effective, board.py:735-787 — exact windowed scan (any board)
 __device__ __forceinline__ bool eff_exact(const Params &P, const int8_t *brd, int a) {
     const int R = P.R, C = P.C, N = P.N;
