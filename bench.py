@@ -227,9 +227,11 @@ def main():
     ap.add_argument("--policy", default="uniform", choices=("uniform", "effective"),
                     help="uniform: random actions over all A (headline); effective: every env samples uniformly "
                          "from its effective actions on device each step (SURVEY §8(d) secondary mode)")
-    ap.add_argument("--phase-blocks", type=int, default=3,
+    ap.add_argument("--phase-blocks", type=int, default=None,
                     help="episode phase blocks: P contiguous env blocks offset by 30/P steps (1 = aligned, "
-                         "0 = every env staggered)")
+                         "0 = every env staggered); default 3, or 1 for --api vector when --steps is a multiple "
+                         "of 30 (a vector env reset once keeps every episode in lock-step, tile_match_env.py:84-101; "
+                         "the window then holds whole reset storms)")
     ap.add_argument("--phase-align", type=int, default=1,
                     help="1: shift the phase blocks so the timed window opens on a block's reset step (0: phases "
                          "from step 0)")
@@ -304,6 +306,8 @@ def main():
     # window of a multiple of `spacing` steps holds the same reset work however
     # it is aligned, but one ending just after a reset times that reset's tail
     # with nothing left to overlap it)
+    if args.phase_blocks is None:
+        args.phase_blocks = 1 if (args.api == "vector" and args.steps % moves == 0) else 3
     spacing = moves // max(1, args.phase_blocks)
     shift = (moves - 1 - args.warmup) % spacing if (args.phase_align and args.phase_blocks > 1
                                                     and not args.phase_interleave) else 0

@@ -30,7 +30,14 @@ namespace tmg {
 
 // Minimum waves per SIMD asked of the register allocator (launch bounds), per
 // kernel; each measured on the MI355X against its neighbours.
-constexpr int kLean128Waves = 7;     // step_kernel<128, false>: the c2 / c4 kernel (72 VGPRs; 8: 64, 1 % slower)
+// step_kernel<128, false>: the c2 / c4 kernel.  8 waves/SIMD (64 VGPRs, no
+// scratch) since round 6 (the row-plane scan freed registers): c4 shard 12.4
+// -> 12.8, c2-eff 4.9 -> 5.0 x 10^8, c2 and its 20-step window the same
+// (profiles/r06/s9); round 5 measured 7 ahead by 1 %.
+#ifndef TMG_LEAN128_WAVES
+#define TMG_LEAN128_WAVES 8
+#endif
+constexpr int kLean128Waves = TMG_LEAN128_WAVES;
 constexpr int kGen128Waves = 5;      // step_kernel<128, true>: c3 (96 VGPRs; 6 / 7 spill and lose, also specialised)
 #ifndef TMG_RESET512_WAVES
 #define TMG_RESET512_WAVES 8
@@ -669,7 +676,10 @@ __device__ __forceinline__ int sample_action(const Params &P, uint64_t effrow, i
     TMG_OPAQUE_V(gid);
     const uint32_t h = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)policy_draw(P.pol_key, gid, P.pol_t));
 #else
-    const uint32_t h = (uint32_t)policy_draw(P.pol_key, (uint64_t)(P.pol_first + e), P.pol_t);
+#ifndef TMG_KO
+#define TMG_KO 0
+#endif
+    const uint32_t h = (TMG_KO & 2) ? (uint32_t)(e * 2654435761u) : (uint32_t)policy_draw(P.pol_key, (uint64_t)(P.pol_first + e), P.pol_t);
 #endif
     const int W = P.W;
     const int pc = __popcll(effrow);                    // 0 on lanes >= W

@@ -413,6 +413,10 @@ __device__ __forceinline__ int sb_ensure(const Params &P, WS &w, int lane, const
             WSYNC();
             dirty = false;
         }
+#ifndef TMG_KO
+#define TMG_KO 0     // diagnostic knock-outs (instruction-count attribution only; results wrong)
+#endif
+        if (TMG_KO & 1) break;
         if ((TMG_RSCAN & 2) && P.C <= kRowScanMaxC ? scan_rows<false>(P, w, lane, true) != 0
                                                     : scan_effective_clean<false>(P, w, lane))
             break;                                           // types all 1, no line
@@ -457,7 +461,7 @@ __device__ __forceinline__ int sb_move(const Params &P, WS &w, int lane, const L
     WSYNC();
     SBC c = sb_codes_from_lds(P, col, lane);
     int elim = 0;
-    for (;;) {                                           // :367-376
+    for (; !(TMG_KO & 4);) {                             // :367-376
         const SBDet d = sb_detect<NB, CODD>(P, sb_planes_of<NB>(c));
         const int rs = sb_bottom_row(P, d);
         if (rs < 0) break;
