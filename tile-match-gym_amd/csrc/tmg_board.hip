@@ -38,6 +38,7 @@ namespace tmg {
 #define TMG_LEAN128_WAVES 8
 #endif
 constexpr int kLean128Waves = TMG_LEAN128_WAVES;
+constexpr int kLean128GenericWaves = 7;   // the generic lean instantiations (8 spills 48-56 B there)
 constexpr int kGen128Waves = 5;      // step_kernel<128, true>: c3 (96 VGPRs; 6 / 7 spill and lose, also specialised)
 #ifndef TMG_RESET512_WAVES
 #define TMG_RESET512_WAVES 8
@@ -2887,7 +2888,8 @@ __device__ __forceinline__ void assume_shape(const Params &P) {
 }
 
 template <int MAXN, bool GEN, int SBNB = 0, bool CODD = false, int FIX = kNoFix>
-__global__ __launch_bounds__(64, MAXN == 128 ? (GEN ? kGen128Waves : kLean128Waves) : (FIX == kFixC5 ? kC5StepWaves : 1)) void step_kernel(
+__global__ __launch_bounds__(64, MAXN == 128 ? (GEN ? kGen128Waves : (FIX != kNoFix ? kLean128Waves : kLean128GenericWaves))
+                                            : (FIX == kFixC5 ? kC5StepWaves : 1)) void step_kernel(
     Params P_, int64_t n, int8_t *__restrict__ board, uint64_t *__restrict__ rng, int32_t *__restrict__ timer,
     const int32_t *__restrict__ actions, int32_t *__restrict__ reward, int32_t *__restrict__ n_new,
     int32_t *__restrict__ n_act, uint8_t *__restrict__ flags_out, uint64_t *__restrict__ eff, int trust_eff,
