@@ -67,24 +67,33 @@ CONFIGS = {
 
 # Profiled runs (tools/issue.py, tools/traffic.py key their counts by these
 # names): a config name runs that config; c4 = BASELINE configs[3], one GPU's
-# shard of 1 048 576 / 8 boards of the c2 shape; a "-eff" suffix adds
-# --policy effective.
+# shard of 1 048 576 / 8 boards of the c2 shape; suffixes: "-p1" adds
+# --phase-blocks 1 (episodes aligned), "-vec" --api vector (aligned episodes),
+# "-eff" --policy effective.
 PROFILE_RUNS = {"c4": ("c2", 131072)}
+SUFFIXES = (("-eff", ["--policy", "effective"]), ("-vec", ["--api", "vector"]), ("-p1", ["--phase-blocks", "1"]))
 
 
 def run_args(name):
     """bench.py arguments of a profiled run name."""
-    base, eff = (name[:-4], True) if name.endswith("-eff") else (name, False)
-    cfg, boards = PROFILE_RUNS.get(base, (base, 0))
-    return ["--config", cfg] + (["--boards", str(boards)] if boards else []) + (["--policy", "effective"] if eff else [])
+    extra = []
+    for suf, args in SUFFIXES:
+        if name.endswith(suf):
+            name, extra = name[:-len(suf)], args + extra
+    cfg, boards = PROFILE_RUNS.get(name, (name, 0))
+    return ["--config", cfg] + (["--boards", str(boards)] if boards else []) + extra
 
 
-def run_name(config, boards, policy):
+def run_name(config, boards, policy, api="raw", phase_blocks=3):
     """The profiled-run name of a bench line (the inverse of run_args)."""
     base = config
     for name, (cfg, nb) in PROFILE_RUNS.items():
         if cfg == config and nb == boards:
             base = name
+    if api == "vector":
+        base += "-vec"
+    elif phase_blocks == 1:
+        base += "-p1"
     return base + ("-eff" if policy == "effective" else "")
 
 
@@ -103,7 +112,8 @@ def run_identity(line):
     library build (source hash), the policy, the run shape and the API."""
     c = line["config"]
     return {"build_src": line["build"]["src"], "policy": c.get("policy", "uniform"), "api": c.get("api", "raw"),
-            "boards_per_gpu": c["boards_per_gpu"], "env_groups_per_gpu": c["env_groups_per_gpu"]}
+            "boards_per_gpu": c["boards_per_gpu"], "env_groups_per_gpu": c["env_groups_per_gpu"],
+            "phase_blocks": c.get("phase_blocks", 3)}
 
 
 def workload_desc(R, C, k, nb, specials):
@@ -401,8 +411,8 @@ def main():
                                                                              policy=args.policy)
         issue = None
         ident = {"build_src": build["src"][:16], "policy": args.policy, "api": args.api, "boards_per_gpu": nb,
-                 "env_groups_per_gpu": env.groups}
-        run = run_name(args.config, nb, args.policy)
+                 "env_groups_per_gpu": env.groups, "phase_blocks": args.phase_blocks}
+        run = run_name(args.config, nb, args.policy, args.api, args.phase_blocks)
         prof = load_profile("issue.json", run, ident)
         if prof:
             per_gpu = value / world
@@ -443,7 +453,8 @@ def main():
                                       f", Gymnasium vector-env step (next-step autoreset, action masks, "
                                       f"{args.obs_dtype} obs)"),
                        "boards_per_gpu": nb, "rows": R, "cols": C, "colours": k,
-                       "specials": cl + co, "env_groups_per_gpu": env.groups, "policy": args.policy,
+                       "specials": cl + co, "env_groups_per_gpu": env.groups, "phase_blocks": args.phase_blocks,
+                       "policy": args.policy,
                        "api": args.api, "graph": bool(graph is not None),
                        "parallelism": f"dp{world} (independent env shards, no collective)"},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
