@@ -148,15 +148,26 @@ static int do_step(tmg_ctx *ctx, Params P, StepArgs a, hipStream_t s) {
     const bool lean = ctx->P.smask == 0 && a.trust_eff;
     const dim3 grid = tmg::env_grid(a.n);
     const int mode = a.autoreset;
-    // the general and 512-cell kernels leave finished boards to a reset launch
-    // masked by FL_RESET, which runs at several times their occupancy
-    const int deferred = mode && (ctx->maxn == 512 || !lean);
+    // the lane-per-board kernel (tmg_lane.h) takes the lean steps of the
+    // shapes it is built for, unless a fused output (one-hot, vector-env
+    // outputs) is asked for
+#ifndef TMG_LANE
+#define TMG_LANE 0
+#endif
+    const bool lanek = TMG_LANE && lean && ctx->maxn == 128 && tmg::lane_shape(P) && !P.oh && !P.vo_term &&
+                       !P.vo_mask && !P.vo_left && !P.vo_final && !P.vo_obs;
+    // the general and 512-cell kernels (and the lane kernel) leave finished
+    // boards to a reset launch masked by FL_RESET, which runs at several
+    // times their occupancy
+    const int deferred = mode && (ctx->maxn == 512 || !lean || lanek);
     if (!lean) {
         int rc = spill_for(ctx, s, a.n, &P.spill, &P.spill_ws);
         if (rc) return rc;
     }
     a.autoreset = mode == 0 ? 0 : mode == 1 ? (deferred ? 2 : 1) : (deferred ? 4 : 3);
-    if (ctx->maxn == 128) {
+    if (lanek) {
+        tmg::launch_step_lane(s, P, a);
+    } else if (ctx->maxn == 128) {
         if (lean) tmg::launch_step_lean128(ctx->sb, grid, s, P, a);
         else if (ctx->sb && (P.C & 1)) tmg::launch_step_gen128_odd(grid, s, P, a);
         else tmg::launch_step_gen128_even(ctx->sb, grid, s, P, a);

@@ -6,6 +6,9 @@
 
 #include "tmg_board.hip"
 #include "tmg_launch.h"
+#if TMG_TU == 1
+#include "tmg_lane.h"
+#endif
 #if TMG_TU == 6
 #include "tmg_aux.hip"      // non-template kernels: one TU only
 #endif
@@ -66,6 +69,55 @@ void effective_one(dim3 grid, hipStream_t s, const Params &P, int64_t n, const i
 }  // namespace
 
 #if TMG_TU == 1
+// The lane-per-board lean step (tmg_lane.h): EPW envs per one-wave
+// workgroup (lane i < EPW = env EPW * group + i), the groups in wg_env's
+// XCD-blocked order.  Each lane keeps kLaneScratch bytes of LDS for a
+// shuffle's index array (the rare path).
+#ifndef TMG_LANE_EPW
+#define TMG_LANE_EPW 64
+#endif
+#ifndef TMG_LANE_WPE
+#define TMG_LANE_WPE 0          // amdgpu_waves_per_eu(WPE, WPE) when > 0
+#endif
+#ifndef TMG_LANE_LDS
+#define TMG_LANE_LDS 0          // extra LDS bytes per workgroup (caps workgroups per CU)
+#endif
+template <int R, int C, int K>
+__global__ __launch_bounds__(64)
+#if TMG_LANE_WPE > 0
+__attribute__((amdgpu_waves_per_eu(TMG_LANE_WPE, TMG_LANE_WPE)))
+#endif
+void lane_step_kernel(Params P_, int64_t n, int8_t *__restrict__ board, uint64_t *__restrict__ rng,
+                      int32_t *__restrict__ timer, int32_t *__restrict__ actions, int32_t *__restrict__ reward,
+                      int32_t *__restrict__ n_new, int32_t *__restrict__ n_act, uint8_t *__restrict__ flags,
+                      uint64_t *__restrict__ eff, int autoreset) {
+    __shared__ uint8_t scratch[64 * kLaneScratch + TMG_LANE_LDS];
+    const Params &P = TMG_KERNARG_PARAMS(P_);
+    const int lane = threadIdx.x & 63;
+    const int64_t e = wg_env() * TMG_LANE_EPW + lane;
+    if (lane >= TMG_LANE_EPW || e >= n) return;
+    const lane::StepIO io{board, rng, timer, actions, reward, n_new, n_act, flags, eff,
+                          P.num_moves, autoreset, P.sample, P.pol_key, P.pol_first, P.pol_t};
+    const uint32_t st = lane::step_env<lane::Board<R, C, K>>(io, e, scratch + lane * kLaneScratch);
+    if (st & lane::LS_INTERNAL) P.status[0] = 1u;
+    if (st & lane::LS_CALLER) P.status[2] = 1u;
+}
+
+bool lane_shape(const Params &P) {
+    return P.smask == 0 && P.R == 10 && P.C == 10 && (P.k == 4 || P.k == 5);
+}
+
+void launch_step_lane(hipStream_t s, const Params &P, const StepArgs &a) {
+    const dim3 grid = env_grid((a.n + TMG_LANE_EPW - 1) / TMG_LANE_EPW);
+    int32_t *act = const_cast<int32_t *>(a.actions);            // the policy writes its draws back
+    if (P.k == 4)
+        hipLaunchKernelGGL((lane_step_kernel<10, 10, 4>), grid, dim3(64), 0, s, P, a.n, a.board, a.rng, a.timer, act,
+                           a.reward, a.n_new, a.n_act, a.flags, a.eff, a.autoreset);
+    else
+        hipLaunchKernelGGL((lane_step_kernel<10, 10, 5>), grid, dim3(64), 0, s, P, a.n, a.board, a.rng, a.timer, act,
+                           a.reward, a.n_new, a.n_act, a.flags, a.eff, a.autoreset);
+}
+
 void launch_step_lean128(bool sb, dim3 grid, hipStream_t s, const Params &P, const StepArgs &a) {
     if (sb && is_shape<kFixC2>(P)) { step_one<128, false, 2, false, kFixC2>(grid, s, P, a); return; }
     if (!sb) step_one<128, false, 0, false>(grid, s, P, a);

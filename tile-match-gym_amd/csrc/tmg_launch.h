@@ -29,6 +29,11 @@ dim3 env_grid(int64_t n);
 // TU 1 — lean step kernels (no specials, cached mask trusted), <= 128 cells;
 // sb: scalar-bitboard variants (C <= 63)
 void launch_step_lean128(bool sb, dim3 grid, hipStream_t s, const Params &P, const StepArgs &a);
+// and the lane-per-board lean step (tmg_lane.h) for the shapes lane_shape
+// accepts; its autoreset codes are the deferred ones (0, 2, 4)
+bool lane_shape(const Params &P);
+void launch_step_lane(hipStream_t s, const Params &P, const StepArgs &a);
+constexpr int kLaneScratch = 128;      // LDS bytes per lane (a shuffle's index array, N <= 128)
 // TU 2 / 3 — general <= 128-cell step kernels, C even / odd (the
 // non-bitboard one lives in TU 2)
 void launch_step_gen128_even(bool sb, dim3 grid, hipStream_t s, const Params &P, const StepArgs &a);

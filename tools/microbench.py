@@ -77,6 +77,22 @@ def main():
         env.timer.zero_()
         pol += timed(lambda: env.step_effective(t), 1)
     res["policy_us"] = statistics.median(pol)
+    # back-to-back launches between one event pair (no host enqueue gap):
+    # device time per launch of 25 quick-exit steps / 25 policy steps
+    steps = {"quick_b2b_us": lambda: [env.step_raw(acts[0]) for _ in range(25)],
+             "normal_b2b_us": lambda: [env.step_raw(acts[t]) for t in range(1, 26)],
+             "policy_b2b_us": lambda: [env.step_effective(t) for t in range(25)]}
+    for name, fn in steps.items():
+        r = []
+        for rep in range(5):
+            env.timer.zero_()
+            if name == "quick_b2b_us":
+                env.eff.zero_()
+            else:
+                env.compute_effective()
+            torch.cuda.synchronize()
+            r += [x / 25 for x in timed(fn, 1)]
+        res[name] = statistics.median(r)
     print({k: round(v, 2) for k, v in res.items()}, flush=True)
 
 
