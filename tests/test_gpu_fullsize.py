@@ -36,19 +36,24 @@ FULL = {
     "c3": (10, 10, 4, 14, 262144, 0),
     "c4": (10, 10, 4, 0, 131072, 3),
     "c5": (20, 20, 6, 15, 262144, 0),
+    "g1": (10, 10, 5, 0, 65536, 0),
+    # one launch of 262 144 envs of the c2 shape (groups = 1): the lane-per-board
+    # kernel with given actions (tmg_capi.hip do_step, TMG_LANE_MIN_ENVS)
+    "c2x4": (10, 10, 4, 0, 262144, 0),
 }
 CASES = [("c2", "uniform"), ("c3", "uniform"), ("c4", "uniform"), ("c5", "uniform"),
-         ("c2", "effective"), ("c5", "effective")]
+         ("c2", "effective"), ("c5", "effective"), ("c4", "effective"), ("g1", "effective"),
+         ("c2x4", "uniform")]
+GROUPS = {"c2x4": 1}
 
 
-def _blocks(n, groups, rs):
+def _blocks(n, rs):
     """Starts of the replayed blocks: both batch edges, both sides of every
-    env-group boundary, four random interior blocks."""
+    phase-block (and env-group) boundary, four random interior blocks."""
     starts = {0, n - BLOCK}
-    for g in range(1, groups):
-        b = g * n // groups
-        starts |= {b - BLOCK // 2}
-    while len(starts) < groups + 5:
+    for j in (1, 2):
+        starts |= {j * n // 3 - BLOCK // 2}
+    while len(starts) < 8:
         starts.add(int(rs.integers(0, n - BLOCK)))
     return sorted(starts)
 
@@ -68,10 +73,11 @@ def test_full_size(name, policy):
     R, C, k, sm, n, rank = FULL[name]
     cl, co = specials(sm)
     envs = shard_range(rank, n)
-    env = TileMatchVecEnv(n, R, C, k, MOVES, cl, co, seeds=shard_seeds(rank, n), device=DEV, groups=3)
+    env = TileMatchVecEnv(n, R, C, k, MOVES, cl, co, seeds=shard_seeds(rank, n), device=DEV,
+                          groups=GROUPS.get(name, 3))
     A = env.num_actions
     rs = np.random.default_rng(sum(FULL[name]))
-    starts = _blocks(n, env.groups, rs)
+    starts = _blocks(n, rs)
     idx = np.concatenate([np.arange(s, s + BLOCK) for s in starts])
     idx_d = torch.from_numpy(idx).to(DEV)
 

@@ -92,3 +92,33 @@ def test_shard_layout_g8_matches_g1(policy):
     parts = [run(shard_range(g, npr), shard_seeds(g, npr)) for g in range(G)]
     for i in range(3):
         assert np.array_equal(np.concatenate([p[i] for p in parts]), whole[i])
+
+
+@pytest.mark.parametrize("k", [4, 5])
+def test_policy_no_autoreset_vs_oracle(k):
+    """The in-kernel policy without autoreset (the lane-per-board kernel's mode
+    0): episodes end at num_moves with an all-zero mask (tile_match_env.py:
+    119-120), and a further step is a caller error that leaves the env as it
+    was (:94-95)."""
+    from oracle.policy_np import sample_effective_np
+    from tile_match_gym_amd.vec_env import TileMatchVecEnv
+    n, M = 3000, 6
+    env = TileMatchVecEnv(n, 10, 10, k, M, seeds=range(500, 500 + n), device=DEV, autoreset=False)
+    o = orc.OracleBatch(10, 10, k, 0, M, env.rng_words().copy(), threads=16)
+    env.reset()
+    o.reset()
+    A = env.num_actions
+    for t in range(M + 2):
+        env.step_effective(t, key=99)
+        env.join()
+        a = sample_effective_np(o.eff, A, 99, 0, t)
+        assert np.array_equal(env.actions.cpu().numpy(), a), f"step {t}: actions"
+        o.step(a, autoreset=False)
+        for f in ("board", "timer", "eff", "reward", "flags"):
+            got = getattr(env, f).cpu().numpy()
+            got = got.view(np.uint64) if f == "eff" else got
+            assert np.array_equal(got, getattr(o, f)), f"step {t}: {f}"
+        assert np.array_equal(env.rng_words(), o.rng), f"step {t}: rng"
+    assert (env.flags.cpu().numpy() == 0x80).all()             # every env stepped past its end
+    assert env.status(clear=True) == 4                          # STATUS_CALLER
+    env.close()

@@ -150,12 +150,20 @@ static int do_step(tmg_ctx *ctx, Params P, StepArgs a, hipStream_t s) {
     const int mode = a.autoreset;
     // the lane-per-board kernel (tmg_lane.h) takes the lean steps of the
     // shapes it is built for, unless a fused output (one-hot, vector-env
-    // outputs) is asked for
+    // outputs) is asked for, when its lanes are busy: the in-kernel policy
+    // (every move effective) or a launch of >= kLaneMinEnvs envs.  With given
+    // actions on smaller launches the wave-per-board kernels are faster (a
+    // lane's wave runs as long as its longest cascade, and at c2's 65 536
+    // envs there is one such wave per SIMD: DESIGN.md §7.7)
 #ifndef TMG_LANE
-#define TMG_LANE 0
+#define TMG_LANE 1
+#endif
+#ifndef TMG_LANE_MIN_ENVS
+#define TMG_LANE_MIN_ENVS 131072
 #endif
     const bool lanek = TMG_LANE && lean && ctx->maxn == 128 && tmg::lane_shape(P) && !P.oh && !P.vo_term &&
-                       !P.vo_mask && !P.vo_left && !P.vo_final && !P.vo_obs;
+                       !P.vo_mask && !P.vo_left && !P.vo_final && !P.vo_obs &&
+                       (P.sample || a.n >= TMG_LANE_MIN_ENVS);
     // the general and 512-cell kernels (and the lane kernel) leave finished
     // boards to a reset launch masked by FL_RESET, which runs at several
     // times their occupancy

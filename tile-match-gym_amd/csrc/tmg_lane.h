@@ -44,22 +44,79 @@ enum : int { LF_DONE = 1, LF_SHUF = 4, LF_RESET = 8, LF_ERR = 0x80 };
 enum : uint32_t { LS_INTERNAL = 1, LS_CALLER = 4 };
 constexpr int kLaneMaxShuffles = 1 << 12;     // kMaxShuffles
 
+// A 128-cell bitboard.  TMG_LANE_W32 (default): four 32-bit words, so a
+// shift is one funnel shift (v_alignbit_b32) per word instead of 64-bit
+// shifts and ORs; otherwise two 64-bit halves.
+#ifndef TMG_LANE_W32
+#define TMG_LANE_W32 1
+#endif
+TMG_LN uint32_t funnel(uint32_t hi, uint32_t lo, int s) {   // ({hi, lo} >> s) & 0xFFFFFFFF, 0 <= s < 32
+#if defined(__HIP_DEVICE_COMPILE__)
+    return __builtin_amdgcn_alignbit(hi, lo, (unsigned)s);
+#else
+    return (uint32_t)((((uint64_t)hi << 32) | lo) >> s);
+#endif
+}
+#if TMG_LANE_W32
+struct B {
+    uint32_t w[4];
+};
+TMG_LN constexpr B from_halves(uint64_t lo, uint64_t hi) {
+    return B{{(uint32_t)lo, (uint32_t)(lo >> 32), (uint32_t)hi, (uint32_t)(hi >> 32)}};
+}
+TMG_LN uint64_t half(B x, int i) { return (uint64_t)x.w[2 * i] | ((uint64_t)x.w[2 * i + 1] << 32); }
+TMG_LN B operator&(B x, B y) { return B{{x.w[0] & y.w[0], x.w[1] & y.w[1], x.w[2] & y.w[2], x.w[3] & y.w[3]}}; }
+TMG_LN B operator|(B x, B y) { return B{{x.w[0] | y.w[0], x.w[1] | y.w[1], x.w[2] | y.w[2], x.w[3] | y.w[3]}}; }
+TMG_LN B operator^(B x, B y) { return B{{x.w[0] ^ y.w[0], x.w[1] ^ y.w[1], x.w[2] ^ y.w[2], x.w[3] ^ y.w[3]}}; }
+TMG_LN B andn(B x, B y) { return B{{x.w[0] & ~y.w[0], x.w[1] & ~y.w[1], x.w[2] & ~y.w[2], x.w[3] & ~y.w[3]}}; }
+TMG_LN bool any(B x) { return (x.w[0] | x.w[1] | x.w[2] | x.w[3]) != 0u; }
+TMG_LN int popc(B x) {
+    return __builtin_popcount(x.w[0]) + __builtin_popcount(x.w[1]) + __builtin_popcount(x.w[2]) +
+           __builtin_popcount(x.w[3]);
+}
+// content moves D cells forward (bit p -> p + D) / back (bit p -> p - D)
+template <int D>
+TMG_LN B fwd(B x) {
+    static_assert(D > 0 && D < 128, "shift");
+    constexpr int q = D >> 5, r = D & 31;
+    B o;
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+        const uint32_t hi = i - q >= 0 ? x.w[i - q] : 0u, lo = i - q - 1 >= 0 ? x.w[i - q - 1] : 0u;
+        o.w[i] = r ? funnel(hi, lo, 32 - r) : hi;
+    }
+    return o;
+}
+template <int D>
+TMG_LN B bwd(B x) {
+    static_assert(D > 0 && D < 128, "shift");
+    constexpr int q = D >> 5, r = D & 31;
+    B o;
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+        const uint32_t lo = i + q <= 3 ? x.w[i + q] : 0u, hi = i + q + 1 <= 3 ? x.w[i + q + 1] : 0u;
+        o.w[i] = r ? funnel(hi, lo, r) : lo;
+    }
+    return o;
+}
+TMG_LN B isolate_lowest(B h) {                    // the lowest set bit of h (h != 0)
+    const uint32_t m0 = h.w[0] & (~h.w[0] + 1u), m1 = h.w[1] & (~h.w[1] + 1u);
+    const uint32_t m2 = h.w[2] & (~h.w[2] + 1u), m3 = h.w[3] & (~h.w[3] + 1u);
+    const bool z0 = h.w[0] == 0u, z1 = z0 && h.w[1] == 0u, z2 = z1 && h.w[2] == 0u;
+    return B{{m0, z0 ? m1 : 0u, z1 ? m2 : 0u, z2 ? m3 : 0u}};
+}
+#else
 struct B {
     uint64_t lo, hi;
 };
+TMG_LN constexpr B from_halves(uint64_t lo, uint64_t hi) { return B{lo, hi}; }
+TMG_LN uint64_t half(B x, int i) { return i ? x.hi : x.lo; }
 TMG_LN B operator&(B x, B y) { return B{x.lo & y.lo, x.hi & y.hi}; }
 TMG_LN B operator|(B x, B y) { return B{x.lo | y.lo, x.hi | y.hi}; }
 TMG_LN B operator^(B x, B y) { return B{x.lo ^ y.lo, x.hi ^ y.hi}; }
 TMG_LN B andn(B x, B y) { return B{x.lo & ~y.lo, x.hi & ~y.hi}; }     // x & ~y
 TMG_LN bool any(B x) { return (x.lo | x.hi) != 0ULL; }
 TMG_LN int popc(B x) { return __builtin_popcountll(x.lo) + __builtin_popcountll(x.hi); }
-TMG_LN int bit(B x, int p) { return (int)(((p < 64 ? x.lo >> p : x.hi >> (p - 64))) & 1ULL); }
-TMG_LN B one(int p) { return p < 64 ? B{1ULL << p, 0} : B{0, 1ULL << (p - 64)}; }
-TMG_LN int lowest(B x) { return x.lo ? __builtin_ctzll(x.lo) : 64 + __builtin_ctzll(x.hi); }       // x != 0
-TMG_LN int highest(B x) { return x.hi ? 127 - __builtin_clzll(x.hi) : 63 - __builtin_clzll(x.lo); } // x != 0
-TMG_LN B drop_lowest(B x) { return x.lo ? B{x.lo & (x.lo - 1), x.hi} : B{0, x.hi & (x.hi - 1)}; }
-
-// content moves D cells forward (bit p -> p + D) / back (bit p -> p - D)
 template <int D>
 TMG_LN B fwd(B x) {
     static_assert(D > 0 && D < 128, "shift");
@@ -72,15 +129,30 @@ TMG_LN B bwd(B x) {
     if constexpr (D >= 64) return B{x.hi >> (D - 64), 0};
     else return B{(x.lo >> D) | (x.hi << (64 - D)), x.hi >> D};
 }
+TMG_LN B isolate_lowest(B h) { return h.lo ? B{h.lo & (~h.lo + 1), 0} : B{0, h.hi & (~h.hi + 1)}; }
+#endif
+// the rarer helpers, on the two 64-bit halves
+TMG_LN int bit(B x, int p) { return (int)((half(x, p >> 6) >> (p & 63)) & 1ULL); }
+TMG_LN B one(int p) { return p < 64 ? from_halves(1ULL << p, 0) : from_halves(0, 1ULL << (p - 64)); }
+TMG_LN int lowest(B x) {                          // x != 0
+    const uint64_t lo = half(x, 0);
+    return lo ? __builtin_ctzll(lo) : 64 + __builtin_ctzll(half(x, 1));
+}
+TMG_LN int highest(B x) {                         // x != 0
+    const uint64_t hi = half(x, 1);
+    return hi ? 127 - __builtin_clzll(hi) : 63 - __builtin_clzll(half(x, 0));
+}
+TMG_LN B drop_lowest(B x) { return x ^ isolate_lowest(x); }
 TMG_LN B fwd_v(B x, int s) {                      // 0 <= s < 128
-    if (s >= 64) return B{0, x.lo << (s - 64)};
+    const uint64_t lo = half(x, 0), hi = half(x, 1);
+    if (s >= 64) return from_halves(0, lo << (s - 64));
     if (s == 0) return x;
-    return B{x.lo << s, (x.hi << s) | (x.lo >> (64 - s))};
+    return from_halves(lo << s, (hi << s) | (lo >> (64 - s)));
 }
 TMG_LN B cells_below(int n) {                     // cells 0..n-1, 0 <= n <= 128
-    if (n >= 128) return B{~0ULL, ~0ULL};
-    if (n >= 64) return B{~0ULL, n == 64 ? 0ULL : (~0ULL >> (128 - n))};
-    return B{n == 0 ? 0ULL : (~0ULL >> (64 - n)), 0};
+    if (n >= 128) return from_halves(~0ULL, ~0ULL);
+    if (n >= 64) return from_halves(~0ULL, n == 64 ? 0ULL : (~0ULL >> (128 - n)));
+    return from_halves(n == 0 ? 0ULL : (~0ULL >> (64 - n)), 0);
 }
 
 // rows r0..r1 x columns c0..c1 of a C-column board (empty when r1 < r0 or c1 < c0)
@@ -92,7 +164,7 @@ TMG_LN constexpr B rect(int C, int r0, int r1, int c0, int c1) {
             if (p < 64) lo |= 1ULL << p;
             else hi |= 1ULL << (p - 64);
         }
-    return B{lo, hi};
+    return from_halves(lo, hi);
 }
 
 // ------------------------------------------------------------------- RNG
@@ -282,7 +354,7 @@ TMG_LN B smear_up(B x) {
 // buffer); with rejections possible, draw by draw.
 template <class BD>
 TMG_LN void deposit(BD &b, B &h, int code) {      // code -> the lowest hole of h, which leaves h
-    const B lb = h.lo ? B{h.lo & (~h.lo + 1), 0} : B{0, h.hi & (~h.hi + 1)};
+    const B lb = isolate_lowest(h);
 #pragma unroll
     for (int k = 0; k < BD::NB; k++)
         if ((code >> k) & 1) b.x[k] = b.x[k] | lb;
@@ -318,9 +390,10 @@ TMG_LN void gravity_refill(BD &b, B E, Rng &g) {
     constexpr int R = BD::R, C = BD::C;
     constexpr B ROW0 = rect(C, 0, 0, 0, C - 1);
     for (;;) {
-        const B below = smear_up<R, C>(E);          // cells with a hole somewhere below
-        const B L = andn(E, below);                 // the lowest hole of each column
-        const B AL = smear_up<R, C>(L);             // the cells above it
+        // cells with a hole somewhere below = the cells above their column's
+        // lowest hole (holes among them)
+        const B AL = smear_up<R, C>(E);
+        const B L = andn(E, AL);                    // the lowest hole of each column
         // settled: no hole has a cell above it that is not a hole
         if (!any(andn(AL, E))) break;
         TMG_LANE_NOTE_PASS();
@@ -337,7 +410,7 @@ TMG_LN void gravity_refill(BD &b, B E, Rng &g) {
 template <class BD>
 TMG_LN void redraw_rows(BD &b, int row, Rng &g) {
     const int M = (row + 1) * BD::C;
-    const B keep = andn(B{~0ULL, ~0ULL}, cells_below(M));
+    const B keep = andn(from_halves(~0ULL, ~0ULL), cells_below(M));
 #pragma unroll
     for (int k = 0; k < BD::NB; k++) b.x[k] = b.x[k] & keep;
     for (int p = 0; p < M; p++) b.set_code(p, draw_code<BD::K>(g));
@@ -374,7 +447,7 @@ TMG_LN void shuffle(BD &b, Rng &g, uint8_t *ix) {
     }
     BD nb;
 #pragma unroll
-    for (int k = 0; k < BD::NB; k++) nb.x[k] = B{0, 0};
+    for (int k = 0; k < BD::NB; k++) nb.x[k] = from_halves(0, 0);
     for (int p = 0; p < N; p++) nb.set_code(p, b.code(ix[p]));
     b = nb;
 }
@@ -411,13 +484,14 @@ TMG_LN void effective_mask(const BD &b, uint64_t *m) {
     const B H = ((uL1 & uL2) | (uU1 & uU2) | (uU1 & uD1) | (uD1 & uD2) |
                  (E2 & E3) | (vU1 & vU2) | (vU1 & Ec1p) | (Ec1p & E2c1p)) & rect(C, 0, R - 1, 0, C - 2);
     // pack: actions 0..AV-1 are V's cells 0..AV-1; action AV + r(C-1) + c is H's cell rC + c
-    uint64_t w[4] = {V.lo, 0, 0, 0};
-    if constexpr (BD::AV > 64) w[1] = V.hi & (~0ULL >> (128 - BD::AV));
+    const uint64_t Vlo = half(V, 0), Vhi = half(V, 1), Hlo = half(H, 0), Hhi = half(H, 1);
+    uint64_t w[4] = {Vlo, 0, 0, 0};
+    if constexpr (BD::AV > 64) w[1] = Vhi & (~0ULL >> (128 - BD::AV));
     else w[0] &= (BD::AV == 64 ? ~0ULL : (~0ULL >> (64 - BD::AV)));
 #pragma unroll
     for (int r = 0; r < R; r++) {
         const int src = r * C, dst = BD::AV + r * (C - 1);
-        const uint64_t row = (src >= 64 ? H.hi >> (src - 64) : ((H.lo >> src) | (src ? H.hi << (64 - src) : 0ULL))) &
+        const uint64_t row = (src >= 64 ? Hhi >> (src - 64) : ((Hlo >> src) | (src ? Hhi << (64 - src) : 0ULL))) &
                              ((1ULL << (C - 1)) - 1ULL);
         const int wi = dst >> 6, off = dst & 63;
         w[wi] |= row << off;
@@ -482,8 +556,9 @@ TMG_LN int move(BD &b, Rng &g, int p1, int p2, int &flags, uint64_t *m, uint8_t 
 template <class BD>
 TMG_LN void unpack(BD &b, const uint64_t *q) {
     constexpr int NQ = (BD::N + 7) / 8;
+    uint64_t lo[BD::NB], hi[BD::NB];
 #pragma unroll
-    for (int k = 0; k < BD::NB; k++) b.x[k] = B{0, 0};
+    for (int k = 0; k < BD::NB; k++) lo[k] = hi[k] = 0;
 #pragma unroll
     for (int i = 0; i < NQ; i++) {
         const uint64_t c = q[i] - 0x0101010101010101ULL;          // colour codes 0..k-1 per byte
@@ -495,10 +570,12 @@ TMG_LN void unpack(BD &b, const uint64_t *q) {
             t |= t >> 28;
             uint64_t v = t & 0xFFULL;
             if (8 * i + 8 > BD::N) v &= (1ULL << (BD::N - 8 * i)) - 1ULL;
-            if (i < 8) b.x[k].lo |= v << (8 * i);
-            else b.x[k].hi |= v << (8 * i - 64);
+            if (i < 8) lo[k] |= v << (8 * i);
+            else hi[k] |= v << (8 * i - 64);
         }
     }
+#pragma unroll
+    for (int k = 0; k < BD::NB; k++) b.x[k] = from_halves(lo[k], hi[k]);
 }
 // the inverse for words 0..nq-1 (the last word's bytes past N are not written by the caller)
 template <class BD>
@@ -506,7 +583,7 @@ TMG_LN uint64_t pack_word(const BD &b, int i) {
     uint64_t w = 0x0101010101010101ULL;
 #pragma unroll
     for (int k = 0; k < BD::NB; k++) {
-        uint64_t v = (i < 8 ? b.x[k].lo >> (8 * i) : b.x[k].hi >> (8 * i - 64)) & 0xFFULL;
+        uint64_t v = (half(b.x[k], i >> 3) >> (8 * (i & 7))) & 0xFFULL;
         v = (v | (v << 28)) & 0x0000000F0000000FULL;
         v = (v | (v << 14)) & 0x0003000300030003ULL;
         v = (v | (v << 7)) & 0x0101010101010101ULL;
