@@ -6,7 +6,7 @@
 #                  so the lines carry them) + the driver-like windows
 #   STAGE=pmcmb  : SQ counts per launch kind (scripts/gpu_r06.sh STAGE=pmcmb)
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
-OUT=$PWD/gpurun_out/r06/final; mkdir -p $OUT
+OUT=$PWD/gpurun_out/r06/${FINAL:-final}; mkdir -p $OUT
 export TMPDIR=/tmp
 PYT="python -u -m pytest -x -v --timeout 300 --timeout-method thread"
 case "${STAGE:-tests}" in
@@ -22,7 +22,7 @@ tests)
   tail -2 $OUT/smoke.log
   ;;
 prof)
-  RUNS="${RUNS:-c2 c2-p1 c2-vec c3 c5 c4 c2-eff c3-eff c5-eff}" bash scripts/gpu_issue.sh
+  RUNS="${RUNS:-c2 c2-p1 c2-vec c3 c5 c4 c2-eff c3-eff c5-eff c4-eff}" bash scripts/gpu_issue.sh
   ;;
 lines)
   run() {   # name, bench args...
@@ -31,13 +31,13 @@ lines)
     tail -1 $OUT/$name.log | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); r=d['roofline']; print('$name', '%.4g' % d['value'], 'ms/step', d['ms_per_step'], 'issue', (r.get('issue') or {}).get('salu_frac'), 'traffic', r.get('traffic_bytes_per_env_step'), 'cpu', (d.get('cpu_baseline') or {}).get('value'))"
   }
   run c2 ; run c2_p1 --phase-blocks 1 ; run c2_vec --api vector ; run c2_eff --policy effective
-  run c3 --config c3 ; run c3_eff --config c3 --policy effective ; run c4 --config c2 --boards 131072
+  run c3 --config c3 ; run c3_eff --config c3 --policy effective ; run c4 --config c2 --boards 131072 ; run c4_eff --config c2 --boards 131072 --policy effective
   run c5 --config c5 ; run c5_eff --config c5 --policy effective ; run g1 --config g1 ; run g2 --config g2
   for i in 1 2 3; do run window20_$i --steps 20 --warmup 5 --no-cpu-baseline; done
   run window40 --steps 40 --warmup 5 --no-cpu-baseline ; run window80 --steps 80 --warmup 5 --no-cpu-baseline
   run gpus2 --gpus 2 --no-cpu-baseline
   ;;
 pmcmb)
-  STAGE=pmcmb TAG=r06/final CONFIGS="${CONFIGS:-c2 c3 c5}" bash scripts/gpu_r06.sh
+  STAGE=pmcmb TAG=r06/${FINAL:-final} CONFIGS="${CONFIGS:-c2 c3 c5}" bash scripts/gpu_r06.sh
   ;;
 esac

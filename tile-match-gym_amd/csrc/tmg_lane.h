@@ -340,12 +340,15 @@ TMG_LN B clear_set(const Det<BD> &d, int rs) {
 // OR of x moved 1..R-1 rows up (bit p -> p - jC)
 template <int R, int C>
 TMG_LN B smear_up(B x) {
-    B s = bwd<C>(x);
-    if constexpr (R > 2) s = s | bwd<C>(s);
-    if constexpr (R > 3) s = s | bwd<2 * C>(s);
-    if constexpr (R > 5) s = s | bwd<4 * C>(s);
-    if constexpr (R > 9) s = s | bwd<8 * C>(s);
-    return s;
+    static_assert(R <= 12, "smear_up covers 11 rows");
+    const B s = bwd<C>(x);
+    if constexpr (R <= 2) return s;
+    else if constexpr (R <= 4) return s | bwd<C>(s) | bwd<2 * C>(s);          // rows 1..3
+    else {
+        const B t = s | bwd<C>(s) | bwd<2 * C>(s);                              // 1..3
+        if constexpr (R <= 10) return t | bwd<3 * C>(t) | bwd<6 * C>(t);        // 1..9
+        else return t | bwd<3 * C>(t) | bwd<6 * C>(t) | bwd<9 * C>(t);          // 1..12 (R <= 12 with 3C < 64, N <= 128)
+    }
 }
 
 // refill (board.py:231-241): the holes h (planes 0 there) take draws in
@@ -550,46 +553,58 @@ TMG_LN int move(BD &b, Rng &g, int p1, int p2, int &flags, uint64_t *m, uint8_t 
 }
 
 // ------------------------------------------------------- board <-> bytes
-// The colour plane of the HBM board (int8 colours 1..k, row-major) in 8-byte
-// words: byte j of word i is cell 8i + j.  Each plane's bit of 8 cells is
-// gathered by three shift-or steps.
+// The colour plane of the HBM board (int8 colours 1..k, row-major), read and
+// written as 8-byte words (byte j of dword i is cell 4i + j).  A plane's bit
+// of 4 cells is one v_dot4_u32_u8 of the masked bytes with (1, 2, 4, 8); the
+// inverse spreads a nibble to the 4 bytes by one multiply.
+TMG_LN uint32_t gather4(uint32_t d) {             // bit 0 of each byte of d -> bits 0..3
+#if defined(__HIP_DEVICE_COMPILE__)
+    return __builtin_amdgcn_udot4(d & 0x01010101u, 0x08040201u, 0u, false);
+#else
+    d &= 0x01010101u;
+    return (d | (d >> 7) | (d >> 14) | (d >> 21)) & 0xFu;
+#endif
+}
+TMG_LN uint32_t spread4(uint32_t n) {             // bits 0..3 of n -> bit 0 of bytes 0..3
+    return (n * 0x00204081u) & 0x01010101u;
+}
 template <class BD>
 TMG_LN void unpack(BD &b, const uint64_t *q) {
-    constexpr int NQ = (BD::N + 7) / 8;
+    constexpr int ND = (BD::N + 3) / 4;
     uint64_t lo[BD::NB], hi[BD::NB];
 #pragma unroll
     for (int k = 0; k < BD::NB; k++) lo[k] = hi[k] = 0;
 #pragma unroll
-    for (int i = 0; i < NQ; i++) {
-        const uint64_t c = q[i] - 0x0101010101010101ULL;          // colour codes 0..k-1 per byte
+    for (int i = 0; i < ND; i++) {
+        const uint64_t qq = q[i >> 1];
+        const uint32_t d = (uint32_t)(i & 1 ? qq >> 32 : qq) - 0x01010101u;   // colour codes 0..k-1 per byte
 #pragma unroll
         for (int k = 0; k < BD::NB; k++) {
-            uint64_t t = (c >> k) & 0x0101010101010101ULL;
-            t |= t >> 7;
-            t |= t >> 14;
-            t |= t >> 28;
-            uint64_t v = t & 0xFFULL;
-            if (8 * i + 8 > BD::N) v &= (1ULL << (BD::N - 8 * i)) - 1ULL;
-            if (i < 8) lo[k] |= v << (8 * i);
-            else hi[k] |= v << (8 * i - 64);
+            uint64_t v = gather4(d >> k);
+            if (4 * i + 4 > BD::N) v &= (1ULL << (BD::N - 4 * i)) - 1ULL;
+            if (i < 16) lo[k] |= v << (4 * i);
+            else hi[k] |= v << (4 * i - 64);
         }
     }
 #pragma unroll
     for (int k = 0; k < BD::NB; k++) b.x[k] = from_halves(lo[k], hi[k]);
 }
-// the inverse for words 0..nq-1 (the last word's bytes past N are not written by the caller)
+// 8-byte word i of the colour plane (cells 8i..8i+7; bytes past N are 1)
 template <class BD>
 TMG_LN uint64_t pack_word(const BD &b, int i) {
-    uint64_t w = 0x0101010101010101ULL;
+    uint32_t d[2];
 #pragma unroll
-    for (int k = 0; k < BD::NB; k++) {
-        uint64_t v = (half(b.x[k], i >> 3) >> (8 * (i & 7))) & 0xFFULL;
-        v = (v | (v << 28)) & 0x0000000F0000000FULL;
-        v = (v | (v << 14)) & 0x0003000300030003ULL;
-        v = (v | (v << 7)) & 0x0101010101010101ULL;
-        w += v << k;
+    for (int j = 0; j < 2; j++) {
+        const int c = 8 * i + 4 * j;                // first cell of the dword
+        uint32_t w = 0x01010101u;
+#pragma unroll
+        for (int k = 0; k < BD::NB; k++) {
+            const uint32_t n = (uint32_t)(half(b.x[k], c >> 6) >> (c & 63)) & 0xFu;
+            w += spread4(n) << k;
+        }
+        d[j] = w;
     }
-    return w;
+    return (uint64_t)d[0] | ((uint64_t)d[1] << 32);
 }
 
 // ------------------------------------------------------------- the policy
@@ -683,9 +698,8 @@ TMG_LN uint32_t step_env(const StepIO &io, int64_t e, uint8_t *scratch) {
     const bool effective = !pend && ((mw[a >> 6] >> (a & 63)) & 1ULL);
     int elim = 0;
     if (effective) {
-        const int8_t *gb = io.board + e * 2 * N;
         BD b;
-        unpack(b, reinterpret_cast<const uint64_t *>(gb));
+        unpack(b, reinterpret_cast<const uint64_t *>(io.board + e * 2 * N));
         Rng g;
         rng_load(g, io.rng + e * 5);
         int r1, c1, r2, c2;
