@@ -72,17 +72,20 @@ void effective_one(dim3 grid, hipStream_t s, const Params &P, int64_t n, const i
 // The lane-per-board lean step (tmg_lane.h): EPW envs per one-wave
 // workgroup (lane i < EPW = env EPW * group + i), the groups in wg_env's
 // XCD-blocked order.  Each lane keeps kLaneScratch bytes of LDS for a
-// shuffle's index array (the rare path).
-#ifndef TMG_LANE_EPW
-#define TMG_LANE_EPW 64
-#endif
+// shuffle's index array (the rare path).  A wave lasts as long as its longest
+// cascade, so a launch too small to give each SIMD two waves of 64 takes 32
+// envs per wave (c2's 21 845-env group launches: c2-eff +4.5 %; at c4's
+// 43 690 the 64-env waves are 4.5 % faster, profiles/r06/s12/).
 #ifndef TMG_LANE_WPE
-#define TMG_LANE_WPE 0          // amdgpu_waves_per_eu(WPE, WPE) when > 0
+#define TMG_LANE_WPE 0          // amdgpu_waves_per_eu(WPE, WPE) when > 0 (A/B)
 #endif
 #ifndef TMG_LANE_LDS
-#define TMG_LANE_LDS 0          // extra LDS bytes per workgroup (caps workgroups per CU)
+#define TMG_LANE_LDS 0          // extra LDS bytes per workgroup (A/B: caps workgroups per CU)
 #endif
-template <int R, int C, int K>
+#ifndef TMG_LANE_SMALL
+#define TMG_LANE_SMALL 32768    // launches below this many envs: 32 envs per wave
+#endif
+template <int R, int C, int K, int EPW>
 __global__ __launch_bounds__(64)
 #if TMG_LANE_WPE > 0
 __attribute__((amdgpu_waves_per_eu(TMG_LANE_WPE, TMG_LANE_WPE)))
@@ -91,11 +94,11 @@ void lane_step_kernel(Params P_, int64_t n, int8_t *__restrict__ board, uint64_t
                       int32_t *__restrict__ timer, int32_t *__restrict__ actions, int32_t *__restrict__ reward,
                       int32_t *__restrict__ n_new, int32_t *__restrict__ n_act, uint8_t *__restrict__ flags,
                       uint64_t *__restrict__ eff, int autoreset) {
-    __shared__ uint8_t scratch[64 * kLaneScratch + TMG_LANE_LDS];
+    __shared__ uint8_t scratch[EPW * kLaneScratch + TMG_LANE_LDS];
     const Params &P = TMG_KERNARG_PARAMS(P_);
     const int lane = threadIdx.x & 63;
-    const int64_t e = wg_env() * TMG_LANE_EPW + lane;
-    if (lane >= TMG_LANE_EPW || e >= n) return;
+    const int64_t e = wg_env() * EPW + lane;
+    if (lane >= EPW || e >= n) return;
     const lane::StepIO io{board, rng, timer, actions, reward, n_new, n_act, flags, eff,
                           P.num_moves, autoreset, P.sample, P.pol_key, P.pol_first, P.pol_t};
     const uint32_t st = lane::step_env<lane::Board<R, C, K>>(io, e, scratch + lane * kLaneScratch);
@@ -107,15 +110,18 @@ bool lane_shape(const Params &P) {
     return P.smask == 0 && P.R == 10 && P.C == 10 && (P.k == 4 || P.k == 5);
 }
 
-void launch_step_lane(hipStream_t s, const Params &P, const StepArgs &a) {
-    const dim3 grid = env_grid((a.n + TMG_LANE_EPW - 1) / TMG_LANE_EPW);
+template <int K, int EPW>
+void lane_one(hipStream_t s, const Params &P, const StepArgs &a) {
+    const dim3 grid = env_grid((a.n + EPW - 1) / EPW);
     int32_t *act = const_cast<int32_t *>(a.actions);            // the policy writes its draws back
-    if (P.k == 4)
-        hipLaunchKernelGGL((lane_step_kernel<10, 10, 4>), grid, dim3(64), 0, s, P, a.n, a.board, a.rng, a.timer, act,
-                           a.reward, a.n_new, a.n_act, a.flags, a.eff, a.autoreset);
-    else
-        hipLaunchKernelGGL((lane_step_kernel<10, 10, 5>), grid, dim3(64), 0, s, P, a.n, a.board, a.rng, a.timer, act,
-                           a.reward, a.n_new, a.n_act, a.flags, a.eff, a.autoreset);
+    hipLaunchKernelGGL((lane_step_kernel<10, 10, K, EPW>), grid, dim3(64), 0, s, P, a.n, a.board, a.rng, a.timer,
+                       act, a.reward, a.n_new, a.n_act, a.flags, a.eff, a.autoreset);
+}
+
+void launch_step_lane(hipStream_t s, const Params &P, const StepArgs &a) {
+    const bool small = a.n < TMG_LANE_SMALL;
+    if (P.k == 4) small ? lane_one<4, 32>(s, P, a) : lane_one<4, 64>(s, P, a);
+    else small ? lane_one<5, 32>(s, P, a) : lane_one<5, 64>(s, P, a);
 }
 
 void launch_step_lean128(bool sb, dim3 grid, hipStream_t s, const Params &P, const StepArgs &a) {
