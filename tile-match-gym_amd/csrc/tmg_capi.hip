@@ -130,10 +130,11 @@ static int set_device(tmg_ctx *ctx) {
 }
 
 static int do_reset(tmg_ctx *ctx, const Params &P, int64_t n, int8_t *board, uint64_t *rng, int32_t *timer,
-                    uint64_t *eff, const uint8_t *env_mask, int mask_bits, hipStream_t s) {
+                    uint64_t *eff, const uint8_t *env_mask, int mask_bits, hipStream_t s, int epw_masked = 0) {
     // a masked reset (the deferred autoreset after every general step; most
     // find no finished env) takes several envs per wave
-    const int epw = !env_mask ? 1 : ctx->maxn == 128 ? tmg::kMaskedResetEnvs128 : tmg::kMaskedResetEnvs512;
+    const int epw = !env_mask ? 1 : epw_masked ? epw_masked
+                  : ctx->maxn == 128 ? tmg::kMaskedResetEnvs128 : tmg::kMaskedResetEnvs512;
     const dim3 grid = tmg::env_grid((n + epw - 1) / epw);
     if (ctx->maxn == 128) tmg::launch_reset128(ctx->sb, grid, s, P, n, board, rng, timer, eff, env_mask, mask_bits, epw);
     else tmg::launch_reset512(grid, s, P, n, board, rng, timer, eff, env_mask, mask_bits, epw);
@@ -191,7 +192,15 @@ static int do_step(tmg_ctx *ctx, Params P, StepArgs a, hipStream_t s) {
         if (rc) return rc;
     }
     if (!deferred) return 0;
-    return do_reset(ctx, P, a.n, a.board, a.rng, a.timer, a.eff, a.flags, tmg::FL_RESET, s);
+    // after a lane step the masked reset takes 2 envs per wave, not 8: the
+    // block storms (a whole env group's regeneration) dominate its time there
+    // (c2-eff 5.45 vs 5.19, c4-eff 9.9 vs 9.45 x 10^8 on one box; 1 / 4 in
+    // between, profiles/r06/s13/)
+#ifndef TMG_LANE_RESET_EPW
+#define TMG_LANE_RESET_EPW 2
+#endif
+    return do_reset(ctx, P, a.n, a.board, a.rng, a.timer, a.eff, a.flags, tmg::FL_RESET, s,
+                    lanek ? TMG_LANE_RESET_EPW : 0);
 }
 
 static int check_call(tmg_ctx *ctx, int64_t n) {
